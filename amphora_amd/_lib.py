@@ -1,0 +1,320 @@
+"""ctypes binding of libamphora_hip.so (the C ABI in include/amphora.h).
+
+This is the product path: every arithmetic call goes to the HIP kernels.
+There is no CPU fallback -- if the shared library is missing or cannot be
+loaded, importing this module raises.
+
+Buffers: host calls take C-contiguous numpy uint8 arrays (or bytes); device
+calls take torch uint8 tensors on the context's GPU and run asynchronously on
+torch's current stream (so torch.cuda.Event timing sees them).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libamphora_hip.so")
+
+AMPH_OK, AMPH_E_VERIFY, AMPH_E_LEN, AMPH_E_PARAM, AMPH_E_HIP, AMPH_E_NOMEM = 0, 1, 2, 3, 4, 5
+AMPH_F_DEVICE = 1
+AMPH_NO_FAILURE = 0x7F7F7F7F7F7F7F7F
+MAX_PARTIES = 16
+
+
+class AmphoraNativeError(RuntimeError):
+    def __init__(self, status: int, detail: str):
+        super().__init__("%s (status %d): %s" % (_STATUS.get(status, "error"), status, detail))
+        self.status = status
+
+
+_STATUS = {AMPH_E_VERIFY: "verification failed", AMPH_E_LEN: "length invariant",
+           AMPH_E_PARAM: "invalid argument", AMPH_E_HIP: "HIP error", AMPH_E_NOMEM: "out of memory"}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libamphora_hip.so not built (%s): run `python -m amphora_amd.build` "
+                          "or __graft_entry__.build(); there is no CPU fallback" % LIB_PATH)
+    # torch (if present) ships its own libamdhip64.so.7; loading it first makes
+    # this library bind to the same HIP runtime instance (same SONAME), so
+    # device pointers and streams from torch are valid here.
+    if "torch" not in sys.modules:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+    L = C.CDLL(LIB_PATH)
+    vp, sz, i32, u32, u64, i64p = C.c_void_p, C.c_size_t, C.c_int, C.c_uint32, C.c_uint64, C.POINTER(C.c_int64)
+    L.amph_ctx_create.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, i32, C.POINTER(vp)]
+    L.amph_ctx_destroy.argtypes = [vp]
+    L.amph_ctx_device.argtypes = [vp]
+    L.amph_ctx_set_batch_words.argtypes = [vp, sz]
+    L.amph_strerror.restype = C.c_char_p
+    L.amph_strerror.argtypes = [i32]
+    L.amph_last_error.restype = C.c_char_p
+    L.amph_version.restype = C.c_char_p
+    L.amph_recombine_verify.argtypes = [vp, vp, i32, vp, i64p, u32, vp]
+    L.amph_mask_input.argtypes = [vp, vp, i32, vp, sz, vp, i64p, u32, vp]
+    L.amph_recombine.argtypes = [vp, C.POINTER(vp), i32, sz, vp, u32, vp]
+    L.amph_verify.argtypes = [vp, vp, vp, vp, vp, vp, sz, i64p, u32, vp]
+    L.amph_verify_message.argtypes = [vp, vp, vp, vp, vp, vp, C.c_char_p, sz]
+    L.amph_mask_words.argtypes = [vp, vp, vp, sz, vp, u32, vp]
+    L.amph_to_gfp.argtypes = [vp, vp, sz, vp, u32, vp]
+    L.amph_from_gfp.argtypes = [vp, vp, sz, vp, u32, vp]
+    L.amph_convert_share.argtypes = [vp, vp, vp, sz, C.c_char_p, i32, vp, u32, vp]
+    L.amph_odo_pre.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp, u32, vp]
+    L.amph_open_diffs.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), i32, sz, vp, u32, vp]
+    L.amph_odo_post.argtypes = [vp, vp, vp, sz, i32, vp, vp, u32, vp]
+    L.amph_synth_odos.argtypes = [vp, u64, i32, sz, C.POINTER(vp), vp, C.c_int64, i32, vp]
+    L.amph_synth_words.argtypes = [vp, u64, sz, vp, vp]
+    return L
+
+
+lib = _load()
+
+EXPORTED = ["amph_ctx_create", "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_set_batch_words",
+            "amph_strerror", "amph_last_error", "amph_version", "amph_recombine_verify",
+            "amph_mask_input", "amph_recombine", "amph_verify", "amph_verify_message",
+            "amph_mask_words", "amph_to_gfp", "amph_from_gfp", "amph_convert_share",
+            "amph_odo_pre", "amph_open_diffs", "amph_odo_post", "amph_synth_odos",
+            "amph_synth_words"]
+
+
+class _AmphOdo(C.Structure):
+    _fields_ = [("secret_shares", C.c_void_p), ("r_shares", C.c_void_p), ("v_shares", C.c_void_p),
+                ("w_shares", C.c_void_p), ("u_shares", C.c_void_p), ("nbytes", C.c_size_t)]
+
+
+def le16(x: int) -> bytes:
+    return int(x).to_bytes(16, "little")
+
+
+def _is_dev(x) -> bool:
+    return hasattr(x, "is_cuda") and x.is_cuda
+
+
+def words_view(x, width: int = 16):
+    """bytes / bytearray / numpy -> C-contiguous uint8 numpy array (n, width)."""
+    if _is_dev(x):
+        return x
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        a = np.frombuffer(bytes(x), np.uint8)
+    else:
+        a = np.ascontiguousarray(x, dtype=np.uint8)
+    n = a.size // width
+    return a.reshape(-1)[: n * width].reshape(n, width)
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if _is_dev(x):
+        return x.data_ptr()
+    return x.ctypes.data
+
+
+class Context:
+    """One amph_ctx: field parameters (prime, r, rInv) bound to one GPU."""
+
+    def __init__(self, prime: int, r: int, r_inv: int, device: int = 0):
+        self.prime, self.r, self.r_inv, self.device = prime, r, r_inv, device
+        h = C.c_void_p()
+        self._check(lib.amph_ctx_create(le16(prime % (1 << 128)), le16(r % (1 << 128)),
+                                        le16(r_inv % (1 << 128)), device, C.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.amph_ctx_destroy(h)
+            self._h = None
+
+    @staticmethod
+    def _check(st: int, allow_verify: bool = False):
+        if st == AMPH_OK or (allow_verify and st == AMPH_E_VERIFY):
+            return st
+        raise AmphoraNativeError(st, lib.amph_last_error().decode())
+
+    def set_batch_words(self, words: int):
+        self._check(lib.amph_ctx_set_batch_words(self._h, words))
+
+    # -- mode plumbing ----------------------------------------------------------
+    def _mode(self, *arrays):
+        dev = [_is_dev(a) for a in arrays if a is not None]
+        if any(dev) and not all(dev):
+            raise ValueError("mix of host and device buffers")
+        if dev and dev[0]:
+            import torch
+            return AMPH_F_DEVICE, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        return 0, None
+
+    def _empty(self, like, shape, dtype="uint8"):
+        if _is_dev(like):
+            import torch
+            return torch.empty(shape, dtype=getattr(torch, dtype), device=like.device)
+        return np.empty(shape, dtype=dtype)
+
+    def _ff(self, like):
+        if _is_dev(like):
+            import torch
+            t = torch.empty(1, dtype=torch.int64, device=like.device)
+            return t, C.cast(C.c_void_p(t.data_ptr()), C.POINTER(C.c_int64))
+        v = C.c_int64(-1)
+        return v, C.pointer(v)
+
+    @staticmethod
+    def _ff_value(ff):
+        if isinstance(ff, C.c_int64):
+            return ff.value
+        return ff  # device tensor: AMPH_NO_FAILURE or index, read by the caller
+
+    def _odo_structs(self, odos):
+        n = len(odos)
+        arr = (_AmphOdo * n)()
+        views = []
+        for j, o in enumerate(odos):
+            fs = [words_view(f) for f in o]
+            views.append(fs)
+            nbytes = fs[0].shape[0] * 16
+            arr[j] = _AmphOdo(*[_ptr(f) for f in fs], nbytes)
+        return arr, views
+
+    # -- client --------------------------------------------------------------
+    def recombine_verify(self, odos):
+        """odos: list over parties of (y, r, v, w, u) word arrays.
+        Returns (canonical secrets (W,16), first_fail) -- first_fail is -1 /
+        index on the host path, an int64[1] device tensor on the device path."""
+        arr, views = self._odo_structs(odos)
+        flags, stream = self._mode(*[f for v in views for f in v])
+        W = views[0][0].shape[0]
+        out = self._empty(views[0][0], (W, 16))
+        ff, ffp = self._ff(views[0][0])
+        self._check(lib.amph_recombine_verify(self._h, arr, len(odos), _ptr(out), ffp, flags,
+                                              stream), allow_verify=True)
+        return out, self._ff_value(ff)
+
+    def mask_input(self, mask_odos, secrets16):
+        arr, views = self._odo_structs(mask_odos)
+        s = words_view(secrets16)
+        flags, stream = self._mode(s, *[f for v in views for f in v])
+        out = self._empty(s, (s.shape[0], 16))
+        ff, ffp = self._ff(s)
+        self._check(lib.amph_mask_input(self._h, arr, len(mask_odos), _ptr(s), s.shape[0],
+                                        _ptr(out), ffp, flags, stream), allow_verify=True)
+        return out, self._ff_value(ff)
+
+    def recombine(self, shares):
+        vs = [words_view(s) for s in shares]
+        flags, stream = self._mode(*vs)
+        W = vs[0].shape[0]
+        out = self._empty(vs[0], (W, 16))
+        ptrs = (C.c_void_p * len(vs))(*[_ptr(v) for v in vs])
+        self._check(lib.amph_recombine(self._h, ptrs, len(vs), W * 16, _ptr(out), flags, stream))
+        return out
+
+    def verify(self, y, r, u, v, w):
+        a = [words_view(x) for x in (y, r, u, v, w)]
+        flags, stream = self._mode(*a)
+        ff, ffp = self._ff(a[0])
+        self._check(lib.amph_verify(self._h, *[_ptr(x) for x in a], a[0].shape[0], ffp, flags,
+                                    stream), allow_verify=True)
+        return self._ff_value(ff)
+
+    def verify_message(self, y: int, r: int, u: int, v: int, w: int) -> str:
+        buf = C.create_string_buffer(1024)
+        n = lib.amph_verify_message(self._h, *[le16(x) for x in (y, r, u, v, w)], buf, 1024)
+        if n < 0:
+            raise AmphoraNativeError(-n, lib.amph_last_error().decode())
+        return buf.value.decode()
+
+    def mask_words(self, secrets16, masks16):
+        s, m = words_view(secrets16), words_view(masks16)
+        flags, stream = self._mode(s, m)
+        out = self._empty(s, (s.shape[0], 16))
+        self._check(lib.amph_mask_words(self._h, _ptr(s), _ptr(m), s.shape[0], _ptr(out), flags,
+                                        stream))
+        return out
+
+    def to_gfp(self, words16):
+        a = words_view(words16)
+        flags, stream = self._mode(a)
+        out = self._empty(a, (a.shape[0], 16))
+        self._check(lib.amph_to_gfp(self._h, _ptr(a), a.shape[0], _ptr(out), flags, stream))
+        return out
+
+    def from_gfp(self, words16):
+        a = words_view(words16)
+        flags, stream = self._mode(a)
+        out = self._empty(a, (a.shape[0], 16))
+        self._check(lib.amph_from_gfp(self._h, _ptr(a), a.shape[0], _ptr(out), flags, stream))
+        return out
+
+    # -- service -------------------------------------------------------------
+    def convert_share(self, masked16, tuples32, mac_key: int, use_zero_input_as_data: bool):
+        m, t = words_view(masked16), words_view(tuples32, 32)
+        flags, stream = self._mode(m, t)
+        out = self._empty(m, (m.shape[0], 32))
+        self._check(lib.amph_convert_share(self._h, _ptr(m), _ptr(t), m.shape[0],
+                                           le16(mac_key % self.prime), int(use_zero_input_as_data),
+                                           _ptr(out), flags, stream))
+        return out
+
+    def odo_pre(self, share_data, share_stride: int, masks32, triples96):
+        sd = words_view(share_data, share_stride)
+        mk, tr = words_view(masks32, 32), words_view(triples96, 96)
+        flags, stream = self._mode(sd, mk, tr)
+        W = sd.shape[0]
+        y, r, v = (self._empty(sd, (W, 16)) for _ in range(3))
+        mag = self._empty(sd, (2 * W, 2, 16))
+        neg = self._empty(sd, (2 * W, 2))
+        self._check(lib.amph_odo_pre(self._h, _ptr(sd), share_stride, _ptr(mk), _ptr(tr), W,
+                                     _ptr(y), _ptr(r), _ptr(v), _ptr(mag), _ptr(neg), flags,
+                                     stream))
+        return y, r, v, mag, neg
+
+    def open_diffs(self, mags, negs):
+        ms = [m if _is_dev(m) else np.ascontiguousarray(m, np.uint8) for m in mags]
+        ns = [n if _is_dev(n) else np.ascontiguousarray(n, np.uint8) for n in negs]
+        flags, stream = self._mode(*ms, *ns)
+        n_pairs = ms[0].shape[0]
+        out = self._empty(ms[0], (n_pairs, 2, 16))
+        pm = (C.c_void_p * len(ms))(*[_ptr(x) for x in ms])
+        pn = (C.c_void_p * len(ns))(*[_ptr(x) for x in ns])
+        self._check(lib.amph_open_diffs(self._h, pm, pn, len(ms), n_pairs, _ptr(out), flags, stream))
+        return out
+
+    def odo_post(self, opened, triples96, is_player0: bool):
+        op = opened if _is_dev(opened) else np.ascontiguousarray(opened, np.uint8)
+        tr = words_view(triples96, 96)
+        flags, stream = self._mode(op, tr)
+        W = tr.shape[0] // 2
+        w, u = self._empty(tr, (W, 16)), self._empty(tr, (W, 16))
+        self._check(lib.amph_odo_post(self._h, _ptr(op), _ptr(tr), W, int(is_player0), _ptr(w),
+                                      _ptr(u), flags, stream))
+        return w, u
+
+    # -- synthetic device inputs (bench / tests) --------------------------------
+    def synth_odos(self, seed: int, n: int, words: int, fault_index: int = -1,
+                   noncanon_permille: int = 0, with_plain: bool = False):
+        """Returns (odos, buffer, plain_y): a (5, n, W, 16) uint8 device
+        tensor, the per-party (y, r, v, w, u) views of it, optional secrets."""
+        import torch
+        buf = torch.empty((5, n, words, 16), dtype=torch.uint8, device="cuda:%d" % self.device)
+        plain = torch.empty((words, 16), dtype=torch.uint8, device=buf.device) if with_plain else None
+        ptrs = (C.c_void_p * (5 * n))(*[buf[k, j].data_ptr() for k in range(5) for j in range(n)])
+        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        self._check(lib.amph_synth_odos(self._h, seed, n, words, ptrs, _ptr(plain), fault_index,
+                                        noncanon_permille, stream))
+        odos = [tuple(buf[k, j] for k in range(5)) for j in range(n)]
+        return odos, buf, plain
+
+    def synth_words(self, seed: int, count: int):
+        import torch
+        out = torch.empty((count, 16), dtype=torch.uint8, device="cuda:%d" % self.device)
+        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        self._check(lib.amph_synth_words(self._h, seed, count, _ptr(out), stream))
+        return out

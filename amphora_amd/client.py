@@ -1,0 +1,157 @@
+"""Host-side mirror of the client arithmetic (amphora-java-client), routed to
+the HIP kernels through the C ABI.
+
+Mirrors:
+* SecretShareUtil            amphora-java-client/.../client/SecretShareUtil.java:33-157
+  (of :48-51, maskInput :65-68, recombineObject :70-90, verifySecrets :102-141)
+* DefaultAmphoraClient.verifyOutputDeliveryObjects :476-505 and the
+  arithmetic of createSecret :150-160 / getSecret :206-217.
+
+Java BigIntegers are Python ints here.  Host-side obligations of the
+boundary: arbitrary ints are reduced mod p before packing into
+16-byte words; canonical outputs are unpacked back to ints.  No field
+arithmetic happens in Python.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import numpy as np
+
+from . import _lib
+from .entities import (IntegrityVerificationException, MaskedInput, MaskedInputData,
+                       OutputDeliveryObject, Secret, WORD_WIDTH)
+
+_MASK128 = (1 << 128) - 1
+
+
+def pack(values: Sequence[int], prime: int = None) -> np.ndarray:
+    """ints -> (W, 16) LE words; reduced mod prime when given (BigInteger.mod)."""
+    if prime is not None:
+        values = [v % prime if (v < 0 or v > _MASK128) else v for v in values]
+    buf = b"".join(int(v).to_bytes(16, "little") for v in values)
+    return np.frombuffer(buf, np.uint8).reshape(-1, 16).copy() if buf else np.zeros((0, 16), np.uint8)
+
+
+def unpack(words) -> List[int]:
+    if hasattr(words, "is_cuda"):
+        words = words.cpu().numpy()
+    b = np.ascontiguousarray(words, np.uint8).tobytes()
+    return [int.from_bytes(b[i:i + 16], "little") for i in range(0, len(b), 16)]
+
+
+class SecretShareUtil:
+    """Client SecretShareUtil; ``of`` keeps the reference factory signature."""
+
+    def __init__(self, ctx: _lib.Context):
+        self._ctx = ctx
+
+    @classmethod
+    def of(cls, prime: int, r: int, r_inv: int, device: int = 0) -> "SecretShareUtil":
+        if prime is None or r is None or r_inv is None:
+            raise TypeError("prime, r and rInv must not be null")  # @NonNull :48-49
+        return cls(_lib.Context(prime, r, r_inv, device))
+
+    @property
+    def prime(self) -> int:
+        return self._ctx.prime
+
+    @property
+    def r(self) -> int:
+        return self._ctx.r
+
+    @property
+    def r_inv(self) -> int:
+        return self._ctx.r_inv
+
+    @property
+    def context(self) -> _lib.Context:
+        return self._ctx
+
+    def mask_input(self, secret: int, input_mask: int) -> MaskedInputData:
+        """maskInput :65-68: MaskedInputData.of(toGfp((secret - inputMask) mod p))."""
+        return self.mask_inputs([secret], [input_mask])[0]
+
+    def mask_inputs(self, secrets: Sequence[int], input_masks: Sequence[int]) -> List[MaskedInputData]:
+        out = self._ctx.mask_words(pack(secrets, self.prime), pack(input_masks, self.prime))
+        return [MaskedInputData.of(bytes(w)) for w in out]
+
+    def recombine_object(self, shares: Sequence[bytes]) -> List[int]:
+        """recombineObject :70-90 (word count from shares[0], trailing bytes ignored)."""
+        if len(shares) == 0:
+            return []
+        W = len(shares[0]) // WORD_WIDTH
+        views = [_lib.words_view(s)[:W] for s in shares]
+        if any(v.shape[0] < W for v in views):
+            raise IndexError("share arrays shorter than the first")
+        return unpack(self._ctx.recombine(views))
+
+    def verify_secrets(self, secrets, rs, us, vs, ws) -> None:
+        """verifySecrets :102-141 (argument order of the Java method)."""
+        n = len(secrets)
+        p = self.prime
+        # host precheck: a w/u outside [0, p) can never equal a reduced product
+        pre = [i for i in range(n) if not (0 <= ws[i] < p and 0 <= us[i] < p)]
+        ok_w = [w if 0 <= w < p else 0 for w in ws]
+        ok_u = [u if 0 <= u < p else 0 for u in us]
+        ff = self._ctx.verify(pack(secrets, p), pack(rs, p), pack(ok_u), pack(vs, p), pack(ok_w))
+        cand = [i for i in ([ff] if ff >= 0 else []) + pre[:1]]
+        if cand:
+            i = min(cand)
+            raise IntegrityVerificationException(
+                self.failure_message(secrets[i], rs[i], us[i], vs[i], ws[i]))
+
+    def failure_message(self, y, r, u, v, w) -> str:
+        """Message of SecretShareUtil.java:116-129; products computed natively."""
+        p = self.prime
+        fits = all(0 <= x <= _MASK128 for x in (y, r, u, v, w))
+        if fits:
+            return self._ctx.verify_message(y, r, u, v, w)
+        msg = self._ctx.verify_message(y % p, r % p, u % p, v % p, w % p)
+        tail = msg.split("\n")[-1]  # "\t{w} = {aw}   &&   {u} = {au}"
+        aw = tail.split("   &&   ")[0].split(" = ")[1]
+        au = tail.split("   &&   ")[1].split(" = ")[1]
+        return ("Verification of secret has failed:\n\t%d = %d * %d   &&   %d = %d * %d\n"
+                "\t%d = %s   &&   %d = %s" % (w, y, r, u, v, r, w, aw, u, au))
+
+
+def _odo_arrays(odos: Sequence[OutputDeliveryObject]):
+    return [tuple(_lib.words_view(f) for f in o.fields()) for o in odos]
+
+
+def verify_output_delivery_objects(util: SecretShareUtil,
+                                   odos: Sequence[OutputDeliveryObject]) -> List[int]:
+    """DefaultAmphoraClient.verifyOutputDeliveryObjects :476-505, fused into one
+    kernel (K_RV): 5 recombines + verify, returns the canonical secrets."""
+    arrays = _odo_arrays(odos)
+    y, ff = util.context.recombine_verify(arrays)
+    if ff >= 0:
+        _raise_for(util, arrays, ff)
+    return unpack(y)
+
+
+def _raise_for(util: SecretShareUtil, arrays, i: int):
+    # re-render the reference message for word i from its recombined values
+    vals = [unpack(util.context.recombine([a[k][i:i + 1] for a in arrays]))[0] for k in range(5)]
+    y, r, v, w, u = vals
+    raise IntegrityVerificationException(util.failure_message(y, r, u, v, w))
+
+
+def create_masked_input(util: SecretShareUtil, secret: Secret,
+                        mask_odos: Sequence[OutputDeliveryObject]) -> MaskedInput:
+    """Arithmetic of DefaultAmphoraClient.createSecret :150-160 fused into one
+    kernel (K_MASK): verify the Input Mask ODOs, then maskInput per word."""
+    arrays = _odo_arrays(mask_odos)
+    W = arrays[0][0].shape[0]
+    if secret.size() > W:
+        raise IndexError("Index %d out of bounds for length %d" % (W, W))
+    masked, ff = util.context.mask_input(arrays, pack(secret.data, util.prime))
+    if ff >= 0:
+        _raise_for(util, arrays, ff)
+    return MaskedInput(secret.secret_id, [MaskedInputData.of(bytes(w)) for w in masked],
+                       list(secret.tags))
+
+
+def get_secret_data(util: SecretShareUtil, odos: Sequence[OutputDeliveryObject]) -> List[int]:
+    """getSecret :206-217 arithmetic (alias of verify_output_delivery_objects)."""
+    return verify_output_delivery_objects(util, odos)

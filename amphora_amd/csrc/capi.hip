@@ -1,0 +1,668 @@
+// C ABI of libamphora_hip (declared in include/amphora.h).
+//
+// Host-pointer calls stream the word arrays through the device in batches
+// (ctx->batch_words, default 4 Mi words): per batch the inputs go HtoD on one
+// of two HIP streams, the kernel runs, the outputs come back DtoH; two
+// device-side slots let batch k+1's copies overlap batch k's kernel.  Verify
+// failures are reported per batch into a device array of first-fail words,
+// read back once at the end.  Device-pointer calls (AMPH_F_DEVICE) launch
+// straight onto the caller's stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/amphora.h"
+#include "kernels.hpp"
+
+using amph::Fp;
+using amph::W4;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int status, const std::string& msg) {
+  g_last_error = msg;
+  return status;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(AMPH_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                   \
+  do {                                                  \
+    hipError_t e_ = (expr);                             \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr);   \
+  } while (0)
+
+typedef unsigned __int128 u128;
+
+u128 ld128(const uint8_t* b) {
+  uint64_t lo, hi;
+  std::memcpy(&lo, b, 8);
+  std::memcpy(&hi, b + 8, 8);
+  return ((u128)hi << 64) | lo;
+}
+
+W4 w4_of(u128 x) {
+  return W4{{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)}};
+}
+
+u128 u128_of(const W4& w) {
+  return ((u128)w.v[3] << 96) | ((u128)w.v[2] << 64) | ((u128)w.v[1] << 32) | w.v[0];
+}
+
+std::string dec(u128 x) {
+  if (x == 0) return "0";
+  char buf[48];
+  int n = 0;
+  while (x) {
+    buf[n++] = (char)('0' + (int)(x % 10));
+    x /= 10;
+  }
+  std::string s(buf, n);
+  std::reverse(s.begin(), s.end());
+  return s;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct amph_ctx {
+  int device = 0;
+  Fp f{};
+  u128 p = 0, r = 0, rinv = 0;
+  std::mutex mu;
+  size_t batch_words = (size_t)4 << 20;
+  int grid_cap = 2048;
+  hipStream_t streams[2] = {nullptr, nullptr};
+  DevBuf slot[2];
+  DevBuf ff;  // per-batch first-fail words (host path)
+};
+
+namespace {
+
+// ---- field setup (host) -----------------------------------------------------
+u128 add_mod(u128 a, u128 b, u128 p) {  // a, b < p
+  u128 s = a + b;
+  if (s < a || s >= p) s -= p;
+  return s;
+}
+
+int setup_field(amph_ctx* c, const uint8_t* p_le, const uint8_t* r_le, const uint8_t* rinv_le) {
+  const u128 p = ld128(p_le), r = ld128(r_le), rinv = ld128(rinv_le);
+  if (p < 3 || (p & 1) == 0) return fail(AMPH_E_PARAM, "prime must be odd and > 2");
+  const u128 R = ((u128)0 - p) % p;  // 2^128 mod p
+  if (r != R) return fail(AMPH_E_PARAM, "r must equal 2^128 mod prime (MP-SPDZ auxiliary modulus)");
+  Fp f{};
+  const W4 pw = w4_of(p);
+  for (int i = 0; i < 4; ++i) f.p[i] = pw.v[i];
+  uint32_t inv = f.p[0];  // Newton: inv = p^-1 mod 2^32
+  for (int i = 0; i < 5; ++i) inv *= 2u - f.p[0] * inv;
+  f.n0 = (uint32_t)(0u - inv);
+  u128 x = R;  // R^2 mod p = R * 2^128 mod p by 128 doublings
+  for (int i = 0; i < 128; ++i) x = add_mod(x, x, p);
+  const W4 r2 = w4_of(x);
+  for (int i = 0; i < 4; ++i) f.r2[i] = r2.v[i];
+  f.big = (p >> 127) != 0;
+  if (rinv >= p) return fail(AMPH_E_PARAM, "rInv must be reduced mod prime");
+  // r * rInv == 1 (mod p): mont_mul(mont_mul(r, rInv), R^2) = r rInv
+  const W4 t = amph::mont_mul(amph::mont_mul(w4_of(r), w4_of(rinv), f), r2, f);
+  if (u128_of(t) != 1) return fail(AMPH_E_PARAM, "rInv must be the inverse of r mod prime");
+  c->f = f;
+  c->p = p;
+  c->r = r;
+  c->rinv = rinv;
+  return AMPH_OK;
+}
+
+u128 mulmod_host(const amph_ctx* c, u128 a, u128 b) {  // a < p
+  return u128_of(amph::mont_mul(amph::mont_mul(w4_of(a), w4_of(b), c->f), amph::r2_word(c->f), c->f));
+}
+
+amph::LaunchCfg cfg(amph_ctx* c, hipStream_t s) { return amph::LaunchCfg{s, c->grid_cap}; }
+
+// ---- host batching ------------------------------------------------------------
+// A batched host call is described by its input and output arrays, each with
+// a per-word byte size; the kernel launcher receives device pointers of one
+// batch.
+struct HostIn {
+  const uint8_t* host;
+  size_t bytes_per_word;
+};
+struct HostOut {
+  uint8_t* host;
+  size_t bytes_per_word;
+};
+
+template <class Launch>
+int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
+                const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
+                Launch&& launch) {
+  if (first_fail) *first_fail = -1;
+  if (words == 0) return AMPH_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  for (int s = 0; s < 2; ++s)
+    if (!c->streams[s]) HIP_TRY(hipStreamCreateWithFlags(&c->streams[s], hipStreamNonBlocking));
+  const size_t bw = std::min(words, c->batch_words);
+  const size_t nb = (words + bw - 1) / bw;
+  size_t per_word = 0;
+  for (auto& i : ins) per_word += i.bytes_per_word;
+  for (auto& o : outs) per_word += o.bytes_per_word;
+  for (int s = 0; s < 2; ++s) {
+    hipError_t e = c->slot[s].ensure(per_word * bw + 256 * (ins.size() + outs.size()));
+    if (e != hipSuccess) return fail(AMPH_E_NOMEM, std::string("device scratch: ") + hipGetErrorString(e));
+  }
+  if (with_ff) {
+    hipError_t e = c->ff.ensure(nb * sizeof(unsigned long long));
+    if (e != hipSuccess) return fail(AMPH_E_NOMEM, "first-fail words");
+    HIP_TRY(hipMemsetAsync(c->ff.p, 0x7F, nb * sizeof(unsigned long long), c->streams[0]));
+    HIP_TRY(hipStreamSynchronize(c->streams[0]));
+  }
+  for (size_t b = 0; b < nb; ++b) {
+    const int s = (int)(b & 1);
+    hipStream_t st = c->streams[s];
+    const size_t base = b * bw, cnt = std::min(bw, words - base);
+    // carve the slot: inputs then outputs, 256-B aligned
+    uint8_t* cur = (uint8_t*)c->slot[s].p;
+    std::vector<const uint4*> din;
+    std::vector<uint4*> dout;
+    for (auto& i : ins) {
+      HIP_TRY(hipMemcpyAsync(cur, i.host + base * i.bytes_per_word, cnt * i.bytes_per_word,
+                             hipMemcpyHostToDevice, st));
+      din.push_back((const uint4*)cur);
+      cur += (cnt * i.bytes_per_word + 255) & ~(size_t)255;
+    }
+    for (auto& o : outs) {
+      dout.push_back((uint4*)cur);
+      cur += (cnt * o.bytes_per_word + 255) & ~(size_t)255;
+    }
+    unsigned long long* ff = with_ff ? (unsigned long long*)c->ff.p + b : nullptr;
+    hipError_t e = launch(din, dout, cnt, ff, cfg(c, st));
+    if (e != hipSuccess) return hip_fail(e, "kernel launch");
+    for (size_t k = 0; k < outs.size(); ++k)
+      HIP_TRY(hipMemcpyAsync(outs[k].host + base * outs[k].bytes_per_word, dout[k],
+                             cnt * outs[k].bytes_per_word, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipStreamSynchronize(c->streams[0]));
+  HIP_TRY(hipStreamSynchronize(c->streams[1]));
+  if (with_ff) {
+    std::vector<unsigned long long> h(nb);
+    HIP_TRY(hipMemcpy(h.data(), c->ff.p, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (size_t b = 0; b < nb; ++b) {
+      if (h[b] != amph::kNoFail) {
+        if (first_fail) *first_fail = (int64_t)(b * bw + h[b]);
+        return AMPH_E_VERIFY;
+      }
+    }
+  }
+  return AMPH_OK;
+}
+
+int check_ctx(amph_ctx* c) { return c ? AMPH_OK : fail(AMPH_E_PARAM, "null context"); }
+
+int odo_words(const amph_odo* odos, int n, size_t* words) {
+  if (!odos || n < 1 || n > AMPH_MAX_PARTIES)
+    return fail(AMPH_E_PARAM, "n_parties must be in [1, 16] with a non-null ODO array");
+  const size_t w = odos[0].nbytes / AMPH_WORD_WIDTH;
+  for (int j = 0; j < n; ++j) {
+    if (odos[j].nbytes / AMPH_WORD_WIDTH < w)
+      return fail(AMPH_E_LEN, "The provided shares must be of the same length");
+    if (w && (!odos[j].secret_shares || !odos[j].r_shares || !odos[j].v_shares ||
+              !odos[j].w_shares || !odos[j].u_shares))
+      return fail(AMPH_E_PARAM, "null ODO field");
+  }
+  *words = w;
+  return AMPH_OK;
+}
+
+const uint8_t* odo_field(const amph_odo& o, int k) {
+  switch (k) {
+    case 0: return o.secret_shares;
+    case 1: return o.r_shares;
+    case 2: return o.v_shares;
+    case 3: return o.w_shares;
+    default: return o.u_shares;
+  }
+}
+
+// device-mode first-fail: reset to the sentinel on the caller's stream
+int reset_ff_dev(int64_t* ff, hipStream_t s) {
+  if (!ff) return fail(AMPH_E_PARAM, "first_fail is required");
+  HIP_TRY(hipMemsetAsync(ff, 0x7F, sizeof(int64_t), s));
+  return AMPH_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+extern "C" {
+
+const char* amph_version(void) { return "amphora_amd 0.1.0 (gfx950)"; }
+
+const char* amph_last_error(void) { return g_last_error.c_str(); }
+
+const char* amph_strerror(int status) {
+  switch (status) {
+    case AMPH_OK: return "ok";
+    case AMPH_E_VERIFY: return "Verification of secret has failed";
+    case AMPH_E_LEN: return "length invariant violated";
+    case AMPH_E_PARAM: return "invalid argument";
+    case AMPH_E_HIP: return "HIP runtime error";
+    case AMPH_E_NOMEM: return "out of memory";
+    default: return "unknown status";
+  }
+}
+
+int amph_ctx_create(const uint8_t p_le[16], const uint8_t r_le[16], const uint8_t rinv_le[16],
+                    int device, amph_ctx** out) {
+  if (!out || !p_le || !r_le || !rinv_le) return fail(AMPH_E_PARAM, "null argument");
+  *out = nullptr;
+  amph_ctx* c = new (std::nothrow) amph_ctx();
+  if (!c) return fail(AMPH_E_NOMEM, "context");
+  int st = setup_field(c, p_le, r_le, rinv_le);
+  if (st != AMPH_OK) {
+    delete c;
+    return st;
+  }
+  c->device = device;
+  if (const char* g = std::getenv("AMPH_GRID_CAP")) c->grid_cap = std::max(1, std::atoi(g));
+  *out = c;
+  return AMPH_OK;
+}
+
+void amph_ctx_destroy(amph_ctx* c) {
+  if (!c) return;
+  if (c->streams[0] || c->slot[0].p || c->ff.p) {
+    (void)hipSetDevice(c->device);
+    for (int s = 0; s < 2; ++s) {
+      if (c->streams[s]) (void)hipStreamSynchronize(c->streams[s]);
+      c->slot[s].release();
+      if (c->streams[s]) (void)hipStreamDestroy(c->streams[s]);
+    }
+    c->ff.release();
+  }
+  delete c;
+}
+
+int amph_ctx_device(const amph_ctx* c) { return c ? c->device : -1; }
+
+int amph_ctx_set_batch_words(amph_ctx* c, size_t words) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (words) c->batch_words = words;
+  return AMPH_OK;
+}
+
+int amph_recombine_verify(amph_ctx* c, const amph_odo* odos, int n, uint8_t* out_secrets,
+                          int64_t* first_fail, uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  size_t W;
+  if (int st = odo_words(odos, n, &W)) return st;
+  if (W && !out_secrets) return fail(AMPH_E_PARAM, "null output");
+  if (flags & AMPH_F_DEVICE) {
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipSetDevice(c->device));
+    if (int st = reset_ff_dev(first_fail, s)) return st;
+    amph::OdoSet set{};
+    for (int k = 0; k < 5; ++k)
+      for (int j = 0; j < n; ++j) set.f[k][j] = (const uint4*)odo_field(odos[j], k);
+    hipError_t e = amph::launch_recombine_verify(set, n, W, (uint4*)out_secrets,
+                                                 (unsigned long long*)first_fail, c->f, cfg(c, s));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_rv");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  std::vector<HostIn> ins;
+  for (int k = 0; k < 5; ++k)
+    for (int j = 0; j < n; ++j) ins.push_back({odo_field(odos[j], k), 16});
+  return run_batched(c, W, ins, {{out_secrets, 16}}, true, first_fail,
+                     [&](auto& din, auto& dout, size_t cnt, unsigned long long* ff,
+                         const amph::LaunchCfg& lc) {
+                       amph::OdoSet set{};
+                       for (int k = 0; k < 5; ++k)
+                         for (int j = 0; j < n; ++j) set.f[k][j] = din[k * n + j];
+                       return amph::launch_recombine_verify(set, n, cnt, dout[0], ff, c->f, lc);
+                     });
+}
+
+int amph_mask_input(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* secrets,
+                    size_t n_secrets, uint8_t* out_masked, int64_t* first_fail, uint32_t flags,
+                    void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  size_t W;
+  if (int st = odo_words(odos, n, &W)) return st;
+  if (n_secrets > W)
+    return fail(AMPH_E_LEN, "more secret words than verified input masks");
+  if (n_secrets && (!secrets || !out_masked)) return fail(AMPH_E_PARAM, "null secrets/output");
+  if (flags & AMPH_F_DEVICE) {
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipSetDevice(c->device));
+    if (int st = reset_ff_dev(first_fail, s)) return st;
+    amph::OdoSet set{};
+    for (int k = 0; k < 5; ++k)
+      for (int j = 0; j < n; ++j) set.f[k][j] = (const uint4*)odo_field(odos[j], k);
+    hipError_t e = amph::launch_mask_input(set, n, W, (const uint4*)secrets, n_secrets,
+                                           (uint4*)out_masked, (unsigned long long*)first_fail,
+                                           c->f, cfg(c, s));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_mask");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  // masked words beyond n_secrets are never produced: verify the tail
+  // separately so every batch has a secret per word.
+  std::vector<HostIn> ins;
+  for (int k = 0; k < 5; ++k)
+    for (int j = 0; j < n; ++j) ins.push_back({odo_field(odos[j], k), 16});
+  ins.push_back({secrets, 16});
+  int st = run_batched(c, n_secrets, ins, {{out_masked, 16}}, true, first_fail,
+                       [&](auto& din, auto& dout, size_t cnt, unsigned long long* ff,
+                           const amph::LaunchCfg& lc) {
+                         amph::OdoSet set{};
+                         for (int k = 0; k < 5; ++k)
+                           for (int j = 0; j < n; ++j) set.f[k][j] = din[k * n + j];
+                         return amph::launch_mask_input(set, n, cnt, din[5 * n], cnt, dout[0],
+                                                        ff, c->f, lc);
+                       });
+  if (st != AMPH_OK || n_secrets == W) return st;
+  // verify-only tail [n_secrets, W): K_RV into a discarded output
+  std::vector<amph_odo> tail(n);
+  const size_t off = n_secrets * 16;
+  for (int j = 0; j < n; ++j)
+    tail[j] = amph_odo{odos[j].secret_shares + off, odos[j].r_shares + off, odos[j].v_shares + off,
+                       odos[j].w_shares + off, odos[j].u_shares + off, (W - n_secrets) * 16};
+  std::vector<uint8_t> sink((W - n_secrets) * 16);
+  std::vector<HostIn> tins;
+  for (int k = 0; k < 5; ++k)
+    for (int j = 0; j < n; ++j) tins.push_back({odo_field(tail[j], k), 16});
+  int64_t tf = -1;
+  st = run_batched(c, W - n_secrets, tins, {{sink.data(), 16}}, true, &tf,
+                   [&](auto& din, auto& dout, size_t cnt, unsigned long long* ff,
+                       const amph::LaunchCfg& lc) {
+                     amph::OdoSet set{};
+                     for (int k = 0; k < 5; ++k)
+                       for (int j = 0; j < n; ++j) set.f[k][j] = din[k * n + j];
+                     return amph::launch_recombine_verify(set, n, cnt, dout[0], ff, c->f, lc);
+                   });
+  if (st == AMPH_E_VERIFY && first_fail) *first_fail = (int64_t)n_secrets + tf;
+  return st;
+}
+
+int amph_recombine(amph_ctx* c, const uint8_t* const* shares, int n, size_t nbytes, uint8_t* out,
+                   uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (!shares || n < 1 || n > AMPH_MAX_PARTIES) return fail(AMPH_E_PARAM, "n_parties must be in [1, 16]");
+  const size_t W = nbytes / AMPH_WORD_WIDTH;
+  if (W && !out) return fail(AMPH_E_PARAM, "null output");
+  for (int j = 0; j < n; ++j)
+    if (W && !shares[j]) return fail(AMPH_E_PARAM, "null share array");
+  if (flags & AMPH_F_DEVICE) {
+    HIP_TRY(hipSetDevice(c->device));
+    amph::ShareSet set{};
+    for (int j = 0; j < n; ++j) set.s[j] = (const uint4*)shares[j];
+    hipError_t e = amph::launch_recombine(set, n, W, (uint4*)out, c->f, cfg(c, (hipStream_t)stream));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_recombine");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  std::vector<HostIn> ins;
+  for (int j = 0; j < n; ++j) ins.push_back({shares[j], 16});
+  return run_batched(c, W, ins, {{out, 16}}, false, nullptr,
+                     [&](auto& din, auto& dout, size_t cnt, unsigned long long*,
+                         const amph::LaunchCfg& lc) {
+                       amph::ShareSet set{};
+                       for (int j = 0; j < n; ++j) set.s[j] = din[j];
+                       return amph::launch_recombine(set, n, cnt, dout[0], c->f, lc);
+                     });
+}
+
+int amph_verify(amph_ctx* c, const uint8_t* y, const uint8_t* r, const uint8_t* u,
+                const uint8_t* v, const uint8_t* w, size_t words, int64_t* first_fail,
+                uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (words && (!y || !r || !u || !v || !w)) return fail(AMPH_E_PARAM, "null input");
+  if (flags & AMPH_F_DEVICE) {
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipSetDevice(c->device));
+    if (int st = reset_ff_dev(first_fail, s)) return st;
+    hipError_t e = amph::launch_verify((const uint4*)y, (const uint4*)r, (const uint4*)u,
+                                       (const uint4*)v, (const uint4*)w, words,
+                                       (unsigned long long*)first_fail, c->f, cfg(c, s));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_verify");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  return run_batched(c, words, {{y, 16}, {r, 16}, {u, 16}, {v, 16}, {w, 16}}, {}, true,
+                     first_fail,
+                     [&](auto& din, auto&, size_t cnt, unsigned long long* ff,
+                         const amph::LaunchCfg& lc) {
+                       return amph::launch_verify(din[0], din[1], din[2], din[3], din[4], cnt, ff,
+                                                  c->f, lc);
+                     });
+}
+
+int amph_verify_message(amph_ctx* c, const uint8_t y[16], const uint8_t r[16], const uint8_t u[16],
+                        const uint8_t v[16], const uint8_t w[16], char* buf, size_t cap) {
+  if (check_ctx(c) || !y || !r || !u || !v || !w) return -AMPH_E_PARAM;
+  const u128 Y = ld128(y) % c->p, R = ld128(r) % c->p, V = ld128(v) % c->p;
+  const u128 Wv = ld128(w), Uv = ld128(u);
+  const u128 aw = mulmod_host(c, Y, R), au = mulmod_host(c, V, R);
+  const std::string m = "Verification of secret has failed:\n\t" + dec(Wv) + " = " + dec(ld128(y)) +
+                        " * " + dec(ld128(r)) + "   &&   " + dec(Uv) + " = " + dec(ld128(v)) +
+                        " * " + dec(ld128(r)) + "\n\t" + dec(Wv) + " = " + dec(aw) +
+                        "   &&   " + dec(Uv) + " = " + dec(au);
+  if (buf && cap) {
+    const size_t k = std::min(cap - 1, m.size());
+    std::memcpy(buf, m.data(), k);
+    buf[k] = 0;
+  }
+  return (int)m.size();
+}
+
+int amph_convert_share(amph_ctx* c, const uint8_t* masked, const uint8_t* tuples, size_t words,
+                       const uint8_t mac_key_le[16], int use_zero, uint8_t* out, uint32_t flags,
+                       void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (!mac_key_le) return fail(AMPH_E_PARAM, "null mac key");
+  if (words && (!masked || !tuples || !out)) return fail(AMPH_E_PARAM, "null buffer");
+  // [alpha] = alpha R mod p, computed once per call on the host
+  const W4 alpha = amph::mont_mul(w4_of(ld128(mac_key_le)), amph::r2_word(c->f), c->f);
+  if (flags & AMPH_F_DEVICE) {
+    HIP_TRY(hipSetDevice(c->device));
+    hipError_t e = amph::launch_convert_share((const uint4*)masked, (const uint4*)tuples, words,
+                                              alpha, use_zero, (uint4*)out, c->f,
+                                              cfg(c, (hipStream_t)stream));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_conv");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  return run_batched(c, words, {{masked, 16}, {tuples, 32}}, {{out, 32}}, false, nullptr,
+                     [&](auto& din, auto& dout, size_t cnt, unsigned long long*,
+                         const amph::LaunchCfg& lc) {
+                       return amph::launch_convert_share(din[0], din[1], cnt, alpha, use_zero,
+                                                         dout[0], c->f, lc);
+                     });
+}
+
+int amph_odo_pre(amph_ctx* c, const uint8_t* share_data, size_t share_stride,
+                 const uint8_t* masks, const uint8_t* triples, size_t words, uint8_t* oy,
+                 uint8_t* orr, uint8_t* ov, uint8_t* omag, uint8_t* oneg, uint32_t flags,
+                 void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (share_stride != 16 && share_stride != 32)
+    return fail(AMPH_E_PARAM, "share_stride must be 16 or 32");
+  if (words && (!share_data || !masks || !triples || !oy || !orr || !ov || !omag || !oneg))
+    return fail(AMPH_E_PARAM, "null buffer");
+  const int sw = (int)(share_stride / 16);
+  if (flags & AMPH_F_DEVICE) {
+    HIP_TRY(hipSetDevice(c->device));
+    hipError_t e = amph::launch_odo_pre((const uint4*)share_data, sw, (const uint4*)masks,
+                                        (const uint4*)triples, words, (uint4*)oy, (uint4*)orr,
+                                        (uint4*)ov, (uint4*)omag, (uint32_t*)oneg, c->f,
+                                        cfg(c, (hipStream_t)stream));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_odo_pre");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  return run_batched(c, words, {{share_data, share_stride}, {masks, 64}, {triples, 192}},
+                     {{oy, 16}, {orr, 16}, {ov, 16}, {omag, 64}, {oneg, 4}}, false, nullptr,
+                     [&](auto& din, auto& dout, size_t cnt, unsigned long long*,
+                         const amph::LaunchCfg& lc) {
+                       return amph::launch_odo_pre(din[0], sw, din[1], din[2], cnt, dout[0],
+                                                   dout[1], dout[2], dout[3],
+                                                   (uint32_t*)dout[4], c->f, lc);
+                     });
+}
+
+int amph_open_diffs(amph_ctx* c, const uint8_t* const* mags, const uint8_t* const* negs, int n,
+                    size_t n_pairs, uint8_t* out, uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (!mags || !negs || n < 1 || n > AMPH_MAX_PARTIES) return fail(AMPH_E_PARAM, "n_parties must be in [1, 16]");
+  if (n_pairs % 2) return fail(AMPH_E_LEN, "n_pairs must be 2 * words");
+  const size_t W = n_pairs / 2;
+  if (W && !out) return fail(AMPH_E_PARAM, "null output");
+  for (int j = 0; j < n; ++j)
+    if (W && (!mags[j] || !negs[j])) return fail(AMPH_E_PARAM, "null diff array");
+  if (flags & AMPH_F_DEVICE) {
+    HIP_TRY(hipSetDevice(c->device));
+    amph::SignedSet set{};
+    for (int j = 0; j < n; ++j) {
+      set.mag[j] = (const uint4*)mags[j];
+      set.neg[j] = (const uint32_t*)negs[j];
+    }
+    hipError_t e = amph::launch_open_diffs(set, n, W, (uint4*)out, c->f, cfg(c, (hipStream_t)stream));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_open");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  std::vector<HostIn> ins;
+  for (int j = 0; j < n; ++j) ins.push_back({mags[j], 64});
+  for (int j = 0; j < n; ++j) ins.push_back({negs[j], 4});
+  return run_batched(c, W, ins, {{out, 64}}, false, nullptr,
+                     [&](auto& din, auto& dout, size_t cnt, unsigned long long*,
+                         const amph::LaunchCfg& lc) {
+                       amph::SignedSet set{};
+                       for (int j = 0; j < n; ++j) {
+                         set.mag[j] = din[j];
+                         set.neg[j] = (const uint32_t*)din[n + j];
+                       }
+                       return amph::launch_open_diffs(set, n, cnt, dout[0], c->f, lc);
+                     });
+}
+
+int amph_odo_post(amph_ctx* c, const uint8_t* opened, const uint8_t* triples, size_t words,
+                  int is_player0, uint8_t* ow, uint8_t* ou, uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (words && (!opened || !triples || !ow || !ou)) return fail(AMPH_E_PARAM, "null buffer");
+  if (flags & AMPH_F_DEVICE) {
+    HIP_TRY(hipSetDevice(c->device));
+    hipError_t e = amph::launch_odo_post((const uint4*)opened, (const uint4*)triples, words,
+                                         is_player0, (uint4*)ow, (uint4*)ou, c->f,
+                                         cfg(c, (hipStream_t)stream));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_odo_post");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  return run_batched(c, words, {{opened, 64}, {triples, 192}}, {{ow, 16}, {ou, 16}}, false,
+                     nullptr,
+                     [&](auto& din, auto& dout, size_t cnt, unsigned long long*,
+                         const amph::LaunchCfg& lc) {
+                       return amph::launch_odo_post(din[0], din[1], cnt, is_player0, dout[0],
+                                                    dout[1], c->f, lc);
+                     });
+}
+
+int amph_to_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, uint32_t flags,
+                void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (words && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
+  if (flags & AMPH_F_DEVICE) {
+    HIP_TRY(hipSetDevice(c->device));
+    hipError_t e = amph::launch_to_gfp((const uint4*)in, words, (uint4*)out, c->f, cfg(c, (hipStream_t)stream));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_to_gfp");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  return run_batched(c, words, {{in, 16}}, {{out, 16}}, false, nullptr,
+                     [&](auto& din, auto& dout, size_t cnt, unsigned long long*,
+                         const amph::LaunchCfg& lc) {
+                       return amph::launch_to_gfp(din[0], cnt, dout[0], c->f, lc);
+                     });
+}
+
+int amph_from_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, uint32_t flags,
+                  void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (words && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
+  if (flags & AMPH_F_DEVICE) {
+    HIP_TRY(hipSetDevice(c->device));
+    hipError_t e = amph::launch_from_gfp((const uint4*)in, words, (uint4*)out, c->f, cfg(c, (hipStream_t)stream));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_from_gfp");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  return run_batched(c, words, {{in, 16}}, {{out, 16}}, false, nullptr,
+                     [&](auto& din, auto& dout, size_t cnt, unsigned long long*,
+                         const amph::LaunchCfg& lc) {
+                       return amph::launch_from_gfp(din[0], cnt, dout[0], c->f, lc);
+                     });
+}
+
+int amph_mask_words(amph_ctx* c, const uint8_t* secrets, const uint8_t* masks, size_t words,
+                    uint8_t* out, uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (words && (!secrets || !masks || !out)) return fail(AMPH_E_PARAM, "null buffer");
+  if (flags & AMPH_F_DEVICE) {
+    HIP_TRY(hipSetDevice(c->device));
+    hipError_t e = amph::launch_mask_words((const uint4*)secrets, (const uint4*)masks, words,
+                                           (uint4*)out, c->f, cfg(c, (hipStream_t)stream));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_mask_words");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  return run_batched(c, words, {{secrets, 16}, {masks, 16}}, {{out, 16}}, false, nullptr,
+                     [&](auto& din, auto& dout, size_t cnt, unsigned long long*,
+                         const amph::LaunchCfg& lc) {
+                       return amph::launch_mask_words(din[0], din[1], cnt, dout[0], c->f, lc);
+                     });
+}
+
+int amph_synth_odos(amph_ctx* c, uint64_t seed, int n, size_t words, uint8_t* const* out_fields,
+                    uint8_t* out_plain_y, int64_t fault_index, int noncanon_permille,
+                    void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (!out_fields || n < 1 || n > AMPH_MAX_PARTIES) return fail(AMPH_E_PARAM, "n_parties must be in [1, 16]");
+  amph::OutSet set{};
+  for (int k = 0; k < 5; ++k)
+    for (int j = 0; j < n; ++j) {
+      if (words && !out_fields[k * n + j]) return fail(AMPH_E_PARAM, "null output field");
+      set.f[k][j] = (uint4*)out_fields[k * n + j];
+    }
+  HIP_TRY(hipSetDevice(c->device));
+  hipError_t e = amph::launch_synth_odos(set, n, words, seed, (uint4*)out_plain_y, fault_index,
+                                         noncanon_permille, c->f, cfg(c, (hipStream_t)stream));
+  return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_synth");
+}
+
+int amph_synth_words(amph_ctx* c, uint64_t seed, size_t count, uint8_t* out, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (count && !out) return fail(AMPH_E_PARAM, "null output");
+  HIP_TRY(hipSetDevice(c->device));
+  hipError_t e = amph::launch_synth_words((uint4*)out, count, seed, c->f, cfg(c, (hipStream_t)stream));
+  return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_synth_words");
+}
+
+}  // extern "C"

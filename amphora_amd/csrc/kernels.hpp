@@ -1,0 +1,92 @@
+// Launch interface of the share-arithmetic kernels (internal to libamphora_hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "field.hpp"
+
+namespace amph {
+
+constexpr int kMaxParties = 16;
+constexpr int kBlock = 256;
+// first_fail sentinel: what hipMemsetAsync(.., 0x7F, 8) leaves behind.
+constexpr unsigned long long kNoFail = 0x7F7F7F7F7F7F7F7FULL;
+
+// SoA word arrays of one OutputDeliveryObject set: f[field][party], field
+// order y (secretShares), r, v, w, u.  Each points at 16-byte words.
+struct OdoSet {
+  const uint4* f[5][kMaxParties];
+};
+
+struct ShareSet {
+  const uint4* s[kMaxParties];
+};
+
+struct SignedSet {  // per party: diff magnitudes (2 words per pair) + sign words
+  const uint4* mag[kMaxParties];
+  const uint32_t* neg[kMaxParties];  // 4 sign bytes per source word (see K_ODO_PRE)
+};
+
+struct LaunchCfg {
+  hipStream_t stream;
+  int grid_cap;  // max workgroups (grid-stride beyond)
+};
+
+// K_RV: recombine 5 fields over n parties, verify w == y r, u == v r,
+// write canonical y (LE16) and atomic-min the first failing index.
+hipError_t launch_recombine_verify(const OdoSet& odo, int n, size_t words, uint4* out_y,
+                                   unsigned long long* first_fail, const Fp& f, const LaunchCfg& c);
+
+// K_MASK: K_RV over Input Mask ODOs fused with maskInput:
+// out[i] = [s_i] - [m_i] for i < n_secrets (s_i any 128-bit LE integer).
+hipError_t launch_mask_input(const OdoSet& odo, int n, size_t words, const uint4* secrets,
+                             size_t n_secrets, uint4* out_masked, unsigned long long* first_fail,
+                             const Fp& f, const LaunchCfg& c);
+
+// recombineObject for one field: canonical sum_j fromGfp(share_j).
+hipError_t launch_recombine(const ShareSet& sh, int n, size_t words, uint4* out, const Fp& f,
+                            const LaunchCfg& c);
+
+// verifySecrets on canonical (LE16) integers: y r == w and v r == u (mod p).
+hipError_t launch_verify(const uint4* y, const uint4* r, const uint4* u, const uint4* v,
+                         const uint4* w, size_t words, unsigned long long* first_fail,
+                         const Fp& f, const LaunchCfg& c);
+
+// K_CONV: masked (16 B) + input-mask tuple (value||mac, 32 B) -> share (value||mac).
+hipError_t launch_convert_share(const uint4* masked, const uint4* tuples, size_t words,
+                                W4 alpha_mont, int use_zero_input, uint4* out, const Fp& f,
+                                const LaunchCfg& c);
+
+// K_ODO_PRE: raw y/r/v copies + signed Beaver diffs.
+hipError_t launch_odo_pre(const uint4* share_data, int share_stride_words, const uint4* masks,
+                          const uint4* triples, size_t words, uint4* out_y, uint4* out_r,
+                          uint4* out_v, uint4* out_mag, uint32_t* out_neg, const Fp& f,
+                          const LaunchCfg& c);
+
+// recombineDiffs: sum over parties of signed diffs mod p -> canonical opened values.
+hipError_t launch_open_diffs(const SignedSet& d, int n, size_t pairs, uint4* out_opened,
+                             const Fp& f, const LaunchCfg& c);
+
+// K_ODO_POST: Beaver product shares from opened (D, E) + triples -> w, u wire words.
+hipError_t launch_odo_post(const uint4* opened, const uint4* triples, size_t words,
+                           int is_player0, uint4* out_w, uint4* out_u, const Fp& f,
+                           const LaunchCfg& c);
+
+// toGfp / fromGfp over word arrays; maskInput with canonical masks.
+hipError_t launch_to_gfp(const uint4* in, size_t words, uint4* out, const Fp& f, const LaunchCfg& c);
+hipError_t launch_from_gfp(const uint4* in, size_t words, uint4* out, const Fp& f, const LaunchCfg& c);
+hipError_t launch_mask_words(const uint4* secrets, const uint4* masks, size_t words, uint4* out,
+                             const Fp& f, const LaunchCfg& c);
+
+// Synthetic honest n-party ODOs (bench/test input generator, device-side).
+struct OutSet {
+  uint4* f[5][kMaxParties];
+};
+hipError_t launch_synth_odos(const OutSet& out, int n, size_t words, uint64_t seed,
+                             uint4* out_plain_y, long long fault_index, int noncanon_permille,
+                             const Fp& f, const LaunchCfg& c);
+hipError_t launch_synth_words(uint4* out, size_t count, uint64_t seed, const Fp& f,
+                              const LaunchCfg& c);
+
+}  // namespace amph

@@ -1,0 +1,205 @@
+"""Benchmark: device-resident share-encode + recombine+verify, secret words/s.
+
+One step = one pass of the hot path over one batch of W words per GPU:
+  K_MASK  createSecret arithmetic: verify the N-party Input Mask ODOs and mask
+          every secret word (DefaultAmphoraClient.java:150-160)
+  K_RV    getSecret arithmetic: recombine the N-party share ODOs and verify
+          the MACs (DefaultAmphoraClient.java:206-217,476-505)
+Inputs are synthetic honest N-party ODOs generated on the device (seeded),
+resident in HBM before the timed region.  Default workload = BASELINE config
+C2: 2^20 words per GPU, 2 parties, the reference's test prime.
+
+Multi-GPU (torchrun, one rank per GPU): each rank owns its own word shard
+(weak scaling, no data-path collective); the per-step verify verdicts are
+combined with one 8-byte RCCL all-reduce(MIN) of the first failing index.
+
+Prints ONE JSON line (rank 0).  Per-kernel HIP-event timings on the launch
+stream feed `roofline`; `cpu_baseline` times the C oracle (a multithreaded
+port of the reference's BigInteger algorithm) on a bounded sample, rank 0 at
+N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "secret words/s device-resident share+recombine, 128-bit prime, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+NO_FAIL = 0x7F7F7F7F7F7F7F7F
+
+
+def kbytes(kernel: str, n: int) -> int:
+    """Algorithmic HBM bytes per word."""
+    return {"k_rv": 80 * n + 16, "k_mask": 80 * n + 32}[kernel]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--words", type=int, default=1 << 20, help="words per GPU (C2: 2^20)")
+    ap.add_argument("--parties", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(n: int, budget_s: float):
+    """Time the C oracle (oracle/amphora_oracle.c: schoolbook multiply + Knuth
+    division per fromGfp/toGfp, like BigInteger) on a bounded sample of the
+    same workload: K_MASK + K_RV arithmetic over W_s words, N parties."""
+    from oracle import coracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    F = coracle.test_field(threads=threads)
+    Ws = 1 << 16
+    mask_odos, _ = F.synth_odos(seed=3, n=n, W=Ws)
+    share_odos, _ = F.synth_odos(seed=4, n=n, W=Ws)
+    secrets = F.synth_words(seed=5, count=Ws, mont=False)
+    F.mask_input(secrets, mask_odos)  # warm-up
+    done, t0 = 0, time.perf_counter()
+    while True:
+        _, f1 = F.mask_input(secrets, mask_odos)
+        _, f2 = F.recombine_verify(share_odos)
+        assert f1 == -1 and f2 == -1
+        done += Ws
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": done / el, "unit": "words/s", "cores": threads, "kind": "port",
+            "sample": "%d words x %d reps (%.1f s): C oracle restating the Java BigInteger "
+                      "path (maskInput+verify on %d-party mask ODOs, recombine+verify on "
+                      "share ODOs), OpenMP %d threads" % (Ws, done // Ws, el, n, n, threads)}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    import amphora_amd as A
+    from oracle.amphora_oracle import TEST_PRIME, TEST_R, TEST_RINV  # constants only
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    ctx = A.Context(TEST_PRIME, TEST_R, TEST_RINV, device=local)
+    W, n = a.words, a.parties
+    mask_odos, mbuf, _ = ctx.synth_odos(seed=1000 + rank, n=n, words=W)
+    share_odos, sbuf, _ = ctx.synth_odos(seed=2000 + rank, n=n, words=W)
+    secrets = ctx.synth_words(seed=3000 + rank, count=W)
+    torch.cuda.synchronize()
+
+    ff = torch.empty(2, dtype=torch.int64, device="cuda")
+    lib = A._lib
+    mask_arr, mviews = ctx._odo_structs(mask_odos)
+    share_arr, sviews = ctx._odo_structs(share_odos)
+    masked = torch.empty((W, 16), dtype=torch.uint8, device="cuda")
+    ys = torch.empty((W, 16), dtype=torch.uint8, device="cuda")
+    import ctypes as C
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ff0 = C.cast(C.c_void_p(ff.data_ptr()), C.POINTER(C.c_int64))
+    ff1 = C.cast(C.c_void_p(ff.data_ptr() + 8), C.POINTER(C.c_int64))
+
+    def k_mask():
+        st = lib.lib.amph_mask_input(ctx._h, mask_arr, n, secrets.data_ptr(), W, masked.data_ptr(),
+                                     ff0, lib.AMPH_F_DEVICE, stream)
+        assert st == 0
+
+    def k_rv():
+        st = lib.lib.amph_recombine_verify(ctx._h, share_arr, n, ys.data_ptr(), ff1,
+                                           lib.AMPH_F_DEVICE, stream)
+        assert st == 0
+
+    verdict = torch.empty(1, dtype=torch.int64, device="cuda")
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        k_mask()
+        if ev is not None:
+            ev[1].record()
+        k_rv()
+        if ev is not None:
+            ev[2].record()
+        if distributed:
+            verdict.copy_(ff.min().view(1))
+            dist.all_reduce(verdict, op=dist.ReduceOp.MIN)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(a.steps):
+        step(events[s])
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    t_mask = sum(e[0].elapsed_time(e[1]) for e in events) / a.steps  # ms per launch
+    t_rv = sum(e[1].elapsed_time(e[2]) for e in events) / a.steps
+    fails = [int(x) for x in ff.cpu().tolist()]
+    if distributed:
+        t = torch.tensor([el, t_mask, t_rv], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, t_mask, t_rv = t.tolist()
+        fails = [int(verdict.cpu().item())]
+    ok = all(f == NO_FAIL for f in fails)
+
+    if rank == 0:
+        ms = el * 1000.0 / a.steps
+        value = W * world * a.steps / el
+        kern = {"k_mask": t_mask, "k_rv": t_rv}
+        dom = max(kern, key=kern.get)
+        bpw = kbytes(dom, n)
+        achieved = bpw * W / (kern[dom] * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(a.traffic_json):
+            try:
+                tj = json.load(open(a.traffic_json))
+                key = "%s_n%d_w%d" % (dom, n, W)
+                traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+            except (ValueError, OSError):
+                traffic = None
+        line = {
+            "metric": METRIC, "value": value, "unit": "words/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u128 mod-p (4x u32 limbs)",
+            "data": "synthetic: device-generated honest %d-party ODOs + secrets (seeded)" % n,
+            "config": {"workload": "C2: K_MASK (share-encode) + K_RV (recombine+verify), "
+                                   "%d words per GPU, %d parties, p = 2^127 < p < 2^128 test prime" % (W, n),
+                       "words_per_gpu": W, "parties": n, "parallelism": "dp%d" % world},
+            "verified": ok,
+            "kernels_ms": {k: round(v, 5) for k, v in kern.items()},
+            "kernels_gbs": {k: round(kbytes(k, n) * W / (v * 1e-3) / 1e9, 1) for k, v in kern.items()},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "bytes_per_word": bpw, "traffic": traffic},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit("verification failed on honest synthetic data: %r" % fails)
+
+
+if __name__ == "__main__":
+    main()

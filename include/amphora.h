@@ -1,0 +1,215 @@
+/*
+ * libamphora_hip -- C ABI of the MI355X-native Amphora share arithmetic.
+ *
+ * The drop-in boundary for the reference's per-word BigInteger path
+ * (carbynestack/amphora, snapshot 2025-03-21; paths relative to the repo):
+ *
+ *   amph_ctx_create      <- client SecretShareUtil.of(prime, r, rInv)
+ *                           amphora-java-client/.../client/SecretShareUtil.java:48-51;
+ *                           service UtilsConfig.java:17-25 (MpSpdzIntegrationUtils.of)
+ *   amph_recombine_verify<- DefaultAmphoraClient.verifyOutputDeliveryObjects
+ *                           amphora-java-client/.../DefaultAmphoraClient.java:476-505
+ *                           (= 5 x SecretShareUtil.recombineObject :70-90
+ *                              + SecretShareUtil.verifySecrets :102-141)
+ *   amph_mask_input      <- DefaultAmphoraClient.createSecret arithmetic :150-160
+ *                           (verifyOutputDeliveryObjects on the Input Mask ODOs
+ *                            + SecretShareUtil.maskInput :65-68 per word)
+ *   amph_recombine       <- SecretShareUtil.recombineObject :70-90
+ *   amph_verify          <- SecretShareUtil.verifySecrets :102-141
+ *   amph_convert_share   <- service calculation/SecretShareUtil.convertToSecretShare
+ *                           amphora-service/.../calculation/SecretShareUtil.java:58-107
+ *   amph_odo_pre         <- OutputDeliveryService.computeOutputDeliveryObject
+ *                           amphora-service/.../calculation/OutputDeliveryService.java:75-139
+ *                           + multiplyShares diff computation :186-200
+ *   amph_open_diffs      <- OutputDeliveryService.recombineDiffs :231-272 (the sum)
+ *   amph_odo_post        <- OutputDeliveryService.multiplySharedSecrets :274-286
+ *                           + w/u encoding :147-152
+ *   amph_mask_words      <- SecretShareUtil.maskInput :65-68 (canonical mask given)
+ *   amph_to_gfp / amph_from_gfp <- MpSpdzIntegrationUtils.toGfp / fromGfp (call
+ *                           sites: client SecretShareUtil.java:56,67; service
+ *                           SecretShareUtil.java:87-104; OutputDeliveryService.java:129-131,150-151)
+ *
+ * Word format: every field element on the wire is 16 bytes, the
+ * mp-spdz-integration 0.2.2 "gfp" encoding toGfp(x) = LE16(x * R mod p),
+ * R = 2^128 (see oracle/amphora_oracle.py, ENCODING "mont_le").  Integers
+ * crossing the ABI in canonical form (secrets, MAC key, opened diffs) are
+ * plain little-endian 16-byte unsigned integers; the host reduces arbitrary
+ * BigIntegers mod p before packing.
+ *
+ * Memory: by default every buffer is a caller-owned HOST pointer; the call is
+ * synchronous and retains nothing.  With AMPH_F_DEVICE every buffer
+ * (including first_fail) is a DEVICE pointer on the context's device, the call
+ * only enqueues work on `stream` (a hipStream_t, NULL = default stream) and
+ * returns; first_fail then holds AMPH_NO_FAILURE or the failing index once the
+ * stream reaches that point.
+ *
+ * Threading: host-pointer calls on one context are serialised by an internal
+ * mutex; device-pointer calls use no context state and may run concurrently.
+ *
+ * Errors: functions return AMPH_OK (0) or a negative/positive status below.
+ * AMPH_E_VERIFY = the MAC check failed; *first_fail then holds the smallest
+ * failing word index (the Java path throws IntegrityVerificationException for
+ * some failing index; see amph_verify_message for the message text).
+ */
+#ifndef AMPHORA_H_
+#define AMPHORA_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AMPH_WORD_WIDTH 16  /* MpSpdzIntegrationUtils.WORD_WIDTH */
+#define AMPH_SHARE_WIDTH 32 /* MpSpdzIntegrationUtils.SHARE_WIDTH (value || mac) */
+#define AMPH_INPUT_MASK_TUPLE_SIZE 32 /* castor INPUT_MASK_GFP tuple: value || mac */
+#define AMPH_TRIPLE_TUPLE_SIZE 96     /* castor MULTIPLICATION_TRIPLE_GFP: a,mac,b,mac,c,mac */
+#define AMPH_MAX_PARTIES 16
+
+/* status codes */
+#define AMPH_OK 0
+#define AMPH_E_VERIFY 1   /* IntegrityVerificationException */
+#define AMPH_E_LEN 2      /* IllegalArgumentException (length invariants) */
+#define AMPH_E_PARAM 3    /* invalid argument / field parameters */
+#define AMPH_E_HIP 4      /* HIP runtime error (see amph_last_error) */
+#define AMPH_E_NOMEM 5    /* device or host allocation failed */
+
+/* flags */
+#define AMPH_F_DEVICE 0x1u /* all buffers are device pointers; async on `stream` */
+
+/* value of a device-side first_fail word when every word verified */
+#define AMPH_NO_FAILURE ((int64_t)0x7F7F7F7F7F7F7F7FLL)
+
+typedef struct amph_ctx amph_ctx;
+
+/* One party's OutputDeliveryObject (amphora-common OutputDeliveryObject.java:55-106):
+ * five byte[] of equal length; words = nbytes / 16 (a trailing partial word
+ * is ignored, as `length / WORD_WIDTH` does in SecretShareUtil.java:75). */
+typedef struct amph_odo {
+  const uint8_t* secret_shares; /* <y>  */
+  const uint8_t* r_shares;      /* <r>  */
+  const uint8_t* v_shares;      /* <v>  */
+  const uint8_t* w_shares;      /* <w> = <y r> */
+  const uint8_t* u_shares;      /* <u> = <v r> */
+  size_t nbytes;
+} amph_odo;
+
+/* ---- context ---------------------------------------------------------- */
+/* p, r = 2^128 mod p, rInv = r^-1 mod p as LE16 integers (SpdzProperties /
+ * DefaultAmphoraClientBuilder.prime/r/rInv).  Checks p odd, r == 2^128 mod p
+ * and r * rInv == 1 (mod p).  `device` = HIP device ordinal. */
+int amph_ctx_create(const uint8_t p_le[16], const uint8_t r_le[16], const uint8_t rinv_le[16],
+                    int device, amph_ctx** out);
+void amph_ctx_destroy(amph_ctx* ctx);
+int amph_ctx_device(const amph_ctx* ctx);
+/* Host-path batch size in words (default 4 Mi); 0 keeps the current value. */
+int amph_ctx_set_batch_words(amph_ctx* ctx, size_t words);
+
+const char* amph_strerror(int status);
+/* Detail of the last error on the calling thread (empty string if none). */
+const char* amph_last_error(void);
+const char* amph_version(void);
+
+/* ---- client (amphora-java-client) ------------------------------------- */
+/* verifyOutputDeliveryObjects: recombine the 5 fields over n_parties ODOs,
+ * check w == y r and u == v r for every word, write the canonical secrets y
+ * (LE16, words = odos[0].nbytes / 16).  Returns AMPH_E_VERIFY with
+ * *first_fail = smallest failing index, else *first_fail = -1 (host mode). */
+int amph_recombine_verify(amph_ctx* ctx, const amph_odo* odos, int n_parties,
+                          uint8_t* out_secrets, int64_t* first_fail, uint32_t flags,
+                          void* stream);
+
+/* createSecret arithmetic: verify the Input Mask ODOs as above and write
+ * masked[i] = toGfp((secret_i - mask_i) mod p) for i < n_secrets.
+ * secrets: LE16 integers (any 128-bit value; reduced mod p).
+ * n_secrets must be <= the ODO word count (else AMPH_E_LEN). */
+int amph_mask_input(amph_ctx* ctx, const amph_odo* mask_odos, int n_parties,
+                    const uint8_t* secrets, size_t n_secrets, uint8_t* out_masked,
+                    int64_t* first_fail, uint32_t flags, void* stream);
+
+/* recombineObject for one byte[] field: out[i] = sum_j fromGfp(share_j[i]) mod p. */
+int amph_recombine(amph_ctx* ctx, const uint8_t* const* shares, int n_parties, size_t nbytes,
+                   uint8_t* out, uint32_t flags, void* stream);
+
+/* verifySecrets over canonical LE16 integers (argument order of the Java
+ * method: secrets, rs, us, vs, ws).  The host must pass w, u < p (a value
+ * outside [0, p) can never equal a reduced product: fail it before calling). */
+int amph_verify(amph_ctx* ctx, const uint8_t* secrets, const uint8_t* rs, const uint8_t* us,
+                const uint8_t* vs, const uint8_t* ws, size_t words, int64_t* first_fail,
+                uint32_t flags, void* stream);
+
+/* Renders the IntegrityVerificationException message of SecretShareUtil.java:116-129
+ * for canonical LE16 values (w, y, r, u, v) of the failing word into buf
+ * (NUL-terminated, truncated to cap).  Returns the untruncated length. */
+int amph_verify_message(amph_ctx* ctx, const uint8_t y[16], const uint8_t r[16],
+                        const uint8_t u[16], const uint8_t v[16], const uint8_t w[16], char* buf,
+                        size_t cap);
+
+/* maskInput word by word with canonical masks (SecretShareUtil.java:65-68):
+ * out[i] = toGfp((secrets[i] - masks[i]) mod p); both LE16 integers. */
+int amph_mask_words(amph_ctx* ctx, const uint8_t* secrets, const uint8_t* masks, size_t words,
+                    uint8_t* out, uint32_t flags, void* stream);
+
+/* MpSpdzIntegrationUtils.toGfp / fromGfp over word arrays (mp-spdz-integration
+ * 0.2.2, absent; restated): toGfp(x) = LE16(x R mod p) for any LE16 integer x;
+ * fromGfp(b) = LEint(b) R^-1 mod p. */
+int amph_to_gfp(amph_ctx* ctx, const uint8_t* in, size_t words, uint8_t* out, uint32_t flags,
+                void* stream);
+int amph_from_gfp(amph_ctx* ctx, const uint8_t* in, size_t words, uint8_t* out, uint32_t flags,
+                  void* stream);
+
+/* ---- service (amphora-service) ---------------------------------------- */
+/* convertToSecretShare: masked (words x 16) + input mask tuples (words x 32,
+ * share 0 value || mac) -> SecretShare.data (words x 32, value || mac).
+ * mac_key: the party's MAC key as an LE16 integer (reduced mod p by the
+ * caller, as new BigInteger(macKey) mod p).  use_zero_input_as_data =
+ * (playerId != 0) in StorageService.createSecret :104-109. */
+int amph_convert_share(amph_ctx* ctx, const uint8_t* masked, const uint8_t* mask_tuples,
+                       size_t words, const uint8_t mac_key_le[16], int use_zero_input_as_data,
+                       uint8_t* out_share, uint32_t flags, void* stream);
+
+/* computeOutputDeliveryObject front half + Beaver diffs.
+ * share_data: words x share_stride bytes (32 = SecretShare.data with MACs,
+ * stripped as in :79-84; 16 = raw words as in InputMaskCachingService :81-91).
+ * mask_tuples: 2*words input-mask tuples (32 B); triples: 2*words triples (96 B).
+ * out_y/out_r/out_v: raw copies (secretShares, rShares, vShares of the ODO).
+ * out_diff_mag: 2*words pairs x 2 values x 16 B, FactorPair order
+ * [d_0, e_0, d_1, e_1, ...]; out_diff_neg: same order, 1 byte each (1 = negative).
+ * Pair 2i = (y_i, r_i), pair 2i+1 = (v_i, r_i); d = x - a, e = y - b,
+ * signed and unreduced, exactly as :186-200. */
+int amph_odo_pre(amph_ctx* ctx, const uint8_t* share_data, size_t share_stride,
+                 const uint8_t* mask_tuples, const uint8_t* triples, size_t words,
+                 uint8_t* out_y, uint8_t* out_r, uint8_t* out_v, uint8_t* out_diff_mag,
+                 uint8_t* out_diff_neg, uint32_t flags, void* stream);
+
+/* recombineDiffs: opened = sum over n_parties signed diff lists (as written
+ * by amph_odo_pre) mod p, canonical LE16, same [D_0, E_0, ...] order.
+ * n_pairs = number of FactorPairs (= 2 * words). */
+int amph_open_diffs(amph_ctx* ctx, const uint8_t* const* diff_mags,
+                    const uint8_t* const* diff_negs, int n_parties, size_t n_pairs,
+                    uint8_t* out_opened, uint32_t flags, void* stream);
+
+/* multiplySharedSecrets + toGfp: per pair k, z = c + D b + E a (+ D E if
+ * is_player0) mod p; out_w[i] = toGfp(z_2i), out_u[i] = toGfp(z_2i+1).
+ * opened: 2*words pairs x 2 canonical LE16 values. */
+int amph_odo_post(amph_ctx* ctx, const uint8_t* opened, const uint8_t* triples, size_t words,
+                  int is_player0, uint8_t* out_w, uint8_t* out_u, uint32_t flags, void* stream);
+
+/* ---- benchmark / test input generation (device pointers only) ---------- */
+/* Honest n-party ODOs: out_fields[k * n_parties + j] = field k (y,r,v,w,u) of
+ * party j (device, words x 16 B each).  out_plain_y (optional, device) gets the
+ * canonical secrets.  fault_index >= 0 adds 1 to party 1's w share there
+ * (party 0 if n_parties == 1); noncanon_permille words per 1000 are written as
+ * [x] + p (when p > 2^127).  Async on `stream`. */
+int amph_synth_odos(amph_ctx* ctx, uint64_t seed, int n_parties, size_t words,
+                    uint8_t* const* out_fields, uint8_t* out_plain_y, int64_t fault_index,
+                    int noncanon_permille, void* stream);
+/* Uniform canonical field elements (LE16), device, async on `stream`. */
+int amph_synth_words(amph_ctx* ctx, uint64_t seed, size_t count, uint8_t* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AMPHORA_H_ */

@@ -1,0 +1,83 @@
+"""CPU-only checks of the C ABI: the library loads, exports every function
+include/amphora.h declares, validates field parameters, and renders the
+reference's verification message (host-side code, no GPU needed)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from oracle import amphora_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P, R, RINV = O.TEST_PRIME, O.TEST_R, O.TEST_RINV
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "amphora.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(amph_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_header(native):
+    lib = ctypes.CDLL(native._lib.LIB_PATH)
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), n
+    assert sorted(native._lib.EXPORTED) == names
+
+
+@pytest.fixture(scope="module")
+def native():
+    import amphora_amd
+    return amphora_amd
+
+
+def test_ctx_param_validation(native):
+    native.Context(P, R, RINV)
+    with pytest.raises(native.AmphoraNativeError, match="r must equal"):
+        native.Context(P, R + 1, RINV)
+    with pytest.raises(native.AmphoraNativeError, match="inverse"):
+        native.Context(P, R, RINV + 1)
+    with pytest.raises(native.AmphoraNativeError, match="odd"):
+        native.Context(P + 1, R, RINV)
+
+
+def test_verify_message_matches_reference_format(native):
+    c = native.Context(P, R, RINV)
+    util = O.ClientSecretShareUtil(P, R, RINV)
+    s, r, v = 123456789, 987654321, 55555
+    w, u = s * r - 10, v * r
+    expected = O.verification_failure_message(P, 0, [s], [r], [u], [v], [w])
+    assert c.verify_message(s, r, u, v, w) == expected
+    big = [P - 1, P - 2, P - 3]
+    exp = O.verification_failure_message(P, 0, [big[0]], [big[1]], [5], [big[2]], [7])
+    assert c.verify_message(big[0], big[1], 5, big[2], 7) == exp
+    assert util  # oracle and native render the same text
+
+
+def test_entities_invariants(native):
+    from amphora_amd import entities as E
+    with pytest.raises(E.IllegalArgumentException, match="same length"):
+        E.OutputDeliveryObject(b"\0" * 16, b"\0" * 16, b"\0" * 32, b"\0" * 16, b"\0" * 16)
+    with pytest.raises(E.IllegalArgumentException, match="has to be 16 bytes"):
+        E.MaskedInputData.of(b"\0" * 15)
+    with pytest.raises(E.IllegalArgumentException, match="multiple of 32"):
+        E.SecretShare(None, b"\0" * 48)
+
+
+def test_name_uuid(native):
+    from amphora_amd.service import name_uuid_from_bytes
+    assert str(name_uuid_from_bytes(b"70297fd4-d412-4dbb-af05-6818fe0e687a_4")) == \
+        "8065e700-9f48-36ba-ae8c-f881b28a28ef"
+
+
+def test_no_gpu_fails_loudly(native):
+    import numpy as np
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    c = native.Context(P, R, RINV)
+    with pytest.raises(native.AmphoraNativeError, match="HIP"):
+        c.recombine_verify([(np.zeros((4, 16), np.uint8),) * 5])

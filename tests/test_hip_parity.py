@@ -1,0 +1,267 @@
+"""Parity of the HIP path (libamphora_hip.so via the C ABI) with the CPU
+oracle.  Bit-exact: this is integer / byte work.
+
+* golden fixtures (tests/golden, produced by the Python oracle, itself pinned
+  to the reference KATs in test_oracle_kat.py) through both the host-pointer
+  and the device-pointer (AMPH_F_DEVICE) entry points;
+* seeded synthetic inputs at sizes the C oracle (oracle/amphora_oracle.c)
+  finishes in seconds, including non-canonical words, faults, ragged sizes,
+  every party count 1..5 and 16, and a prime below 2^127;
+* BASELINE sizes (C2 1 Mi x 2 parties, C3 16 Mi x 3 parties) through
+  size-independent properties: verify passes on honest input, the injected
+  fault is found at its index, and random word samples match the oracle.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from oracle import amphora_oracle as O  # noqa: E402
+from oracle import coracle  # noqa: E402
+
+P, R, RINV = O.TEST_PRIME, O.TEST_R, O.TEST_RINV
+NO_FAIL = 0x7F7F7F7F7F7F7F7F
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need a GPU"
+    return t
+
+
+@pytest.fixture(scope="module")
+def ctx(torch):
+    import amphora_amd as A
+    return A.Context(P, R, RINV, device=0)
+
+
+@pytest.fixture(scope="module")
+def F():
+    return coracle.test_field(threads=16)
+
+
+def _cases(golden_dir):
+    with open(os.path.join(golden_dir, "manifest.json")) as f:
+        return json.load(f)["cases"]
+
+
+def dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def ff_dev(t):
+    v = int(t.cpu().item())
+    return -1 if v == NO_FAIL else v
+
+
+@pytest.mark.parametrize("idx", range(4))
+@pytest.mark.parametrize("mode", ["host", "device"])
+def test_golden(golden_dir, ctx, torch, idx, mode):
+    case = _cases(golden_dir)[idx]
+    d = np.load(os.path.join(golden_dir, case["file"]), allow_pickle=False)
+    n = case["parties"]
+    on = (lambda a: dev(torch, a)) if mode == "device" else (lambda a: np.ascontiguousarray(a))
+    back = host if mode == "device" else (lambda a: a)
+    ffv = ff_dev if mode == "device" else (lambda v: v)
+    for tag in ("honest", "fault", "noncanon"):
+        buf = d["rv_%s_odo" % tag]
+        odos = [tuple(on(buf[k, j]) for k in range(5)) for j in range(n)]
+        y, ff = ctx.recombine_verify(odos)
+        assert ffv(ff) == d["rv_%s_first_fail" % tag][0], tag
+        assert np.array_equal(back(y), d["rv_%s_secrets" % tag]), tag
+    mo = d["mask_odo"]
+    out, ff = ctx.mask_input([tuple(on(mo[k, j]) for k in range(5)) for j in range(n)],
+                             on(d["mask_secrets"]))
+    assert ffv(ff) == -1 and np.array_equal(back(out), d["mask_out"])
+    mf = d["mask_fault_odo"]
+    _, ff = ctx.mask_input([tuple(on(mf[k, j]) for k in range(5)) for j in range(n)],
+                           on(d["mask_secrets"]))
+    assert ffv(ff) == d["mask_fault_first_fail"][0]
+    key = int.from_bytes(d["conv_mac_key"].tobytes(), "little")
+    for z in (0, 1):
+        out = ctx.convert_share(on(d["conv_masked"]), on(d["conv_tuples"]), key, bool(z))
+        assert np.array_equal(back(out), d["conv_out_zero%d" % z])
+    y, r, v, mag, neg = ctx.odo_pre(on(d["odo_share_data"]), 32, on(d["odo_masks"]),
+                                    on(d["odo_triples"]))
+    for got, k in ((y, "odo_y"), (r, "odo_r"), (v, "odo_v"), (mag, "odo_diff_mag"),
+                   (neg, "odo_diff_neg")):
+        assert np.array_equal(back(got), d[k]), k
+    mags = [on(d["odo_diff_mag"])] + [on(d["odo_partner_mag"][j]) for j in range(n - 1)]
+    negs = [on(d["odo_diff_neg"])] + [on(d["odo_partner_neg"][j]) for j in range(n - 1)]
+    assert np.array_equal(back(ctx.open_diffs(mags, negs)), d["odo_opened"])
+    for pid in (0, 1):
+        w, u = ctx.odo_post(on(d["odo_opened"]), on(d["odo_triples"]), pid == 0)
+        assert np.array_equal(back(w), d["odo_w_p%d" % pid])
+        assert np.array_equal(back(u), d["odo_u_p%d" % pid])
+
+
+@pytest.mark.parametrize("n,W", [(1, 777), (2, 100_003), (3, 65_536), (4, 4097), (5, 3000),
+                                 (16, 513)])
+def test_recombine_verify_vs_c_oracle(ctx, F, n, W):
+    odos, _ = F.synth_odos(seed=100 + n, n=n, W=W, noncanon_permille=30)
+    y, ff = ctx.recombine_verify(odos)
+    oy, off = F.recombine_verify(odos)
+    assert ff == off == -1 and np.array_equal(y, oy)
+    fault = W // 3
+    odos, _ = F.synth_odos(seed=200 + n, n=n, W=W, fault_index=fault)
+    y, ff = ctx.recombine_verify(odos)
+    oy, off = F.recombine_verify(odos)
+    assert ff == off == fault and np.array_equal(y, oy)
+
+
+@pytest.mark.parametrize("n,W", [(1, 1000), (2, 262_145), (3, 40_000), (6, 999)])
+def test_mask_input_vs_c_oracle(ctx, F, n, W):
+    odos, _ = F.synth_odos(seed=300 + n, n=n, W=W, noncanon_permille=10)
+    secrets = F.synth_words(seed=7, count=W, mont=False)
+    secrets[::7] = 0xFF  # raw 128-bit integers >= p are reduced too
+    out, ff = ctx.mask_input(odos, secrets)
+    oo, off = F.mask_input(secrets, odos)
+    assert ff == off == -1 and np.array_equal(out, oo)
+
+
+def test_mask_input_fewer_secrets_than_masks(ctx, F):
+    odos, _ = F.synth_odos(seed=11, n=2, W=5000, fault_index=4500)
+    secrets = F.synth_words(seed=8, count=3000, mont=False)
+    out, ff = ctx.mask_input(odos, secrets)
+    assert ff == 4500  # the verify covers every mask word
+    odos, _ = F.synth_odos(seed=11, n=2, W=5000)
+    out, ff = ctx.mask_input(odos, secrets)
+    oo, _ = F.mask_input(secrets, [tuple(f[:3000] for f in o) for o in odos])
+    assert ff == -1 and np.array_equal(out, oo)
+
+
+def test_host_batches_report_global_index(ctx, F):
+    odos, _ = F.synth_odos(seed=12, n=3, W=2500, fault_index=1777)
+    ctx.set_batch_words(1000)
+    try:
+        y, ff = ctx.recombine_verify(odos)
+        oy, _ = F.recombine_verify(odos)
+    finally:
+        ctx.set_batch_words(4 << 20)
+    assert ff == 1777 and np.array_equal(y, oy)
+
+
+def test_empty_and_single(ctx):
+    z = np.zeros((0, 16), np.uint8)
+    y, ff = ctx.recombine_verify([(z,) * 5, (z,) * 5])
+    assert y.shape == (0, 16) and ff == -1
+    assert ctx.recombine([z, z]).shape == (0, 16)
+    out = ctx.convert_share(z, np.zeros((0, 32), np.uint8), 5, False)
+    assert out.shape == (0, 32)
+
+
+def test_party_kernels_vs_c_oracle(ctx, F):
+    W = 50_001
+    masked = F.synth_words(seed=21, count=W)
+    tuples = F.synth_words(seed=22, count=2 * W).reshape(W, 32)
+    key = 123456789123456789123456789 % P
+    for z in (False, True):
+        assert np.array_equal(ctx.convert_share(masked, tuples, key, z),
+                              F.convert_share(masked, tuples, key, z))
+    share = ctx.convert_share(masked, tuples, key, False)
+    masks = F.synth_words(seed=23, count=4 * W).reshape(2 * W, 32)
+    triples = F.synth_words(seed=24, count=12 * W).reshape(2 * W, 96)
+    for stride, data in ((32, share), (16, masked)):
+        got = ctx.odo_pre(data, stride, masks, triples)
+        exp = F.odo_pre(data, stride, masks, triples)
+        for g, e in zip(got, exp):
+            assert np.array_equal(g, e)
+    _, _, _, mag, neg = got
+    pm = F.synth_words(seed=25, count=4 * W).reshape(2 * W, 2, 16)
+    pn = (F.synth_words(seed=26, count=W)[:, :4].reshape(2 * W, 2) & 1).astype(np.uint8)
+    opened = ctx.open_diffs([mag, pm], [neg, pn])
+    assert np.array_equal(opened, F.recombine_diffs([mag, pm], [neg, pn]))
+    for p0 in (True, False):
+        w, u = ctx.odo_post(opened, triples, p0)
+        ew, eu = F.odo_post(opened, triples, p0)
+        assert np.array_equal(w, ew) and np.array_equal(u, eu)
+
+
+def test_codec_and_mask_words(ctx, F):
+    W = 10_000
+    x = F.synth_words(seed=31, count=W, mont=False)
+    x[::5] = 0xFF
+    g = ctx.to_gfp(x)
+    spdz = O.MpSpdzIntegrationUtils(P, R, RINV)
+    xs = [int.from_bytes(w.tobytes(), "little") for w in x[:500]]
+    assert [bytes(w) for w in g[:500]] == [spdz.to_gfp(v) for v in xs]
+    back = ctx.from_gfp(g)
+    assert [int.from_bytes(w.tobytes(), "little") for w in back[:500]] == [v % P for v in xs]
+    m = F.synth_words(seed=32, count=W, mont=False)
+    mw = ctx.mask_words(x, m)
+    ms = [int.from_bytes(w.tobytes(), "little") for w in m[:500]]
+    assert [bytes(w) for w in mw[:500]] == [spdz.to_gfp((a - b) % P) for a, b in zip(xs, ms)]
+
+
+def test_small_prime_path(torch, F):
+    """p = 2^89 - 1 < 2^127: the !BIG canonicalisation path."""
+    import amphora_amd as A
+    p = 2 ** 89 - 1
+    r = pow(2, 128, p)
+    rinv = pow(r, -1, p)
+    c = A.Context(p, r, rinv)
+    Fs = coracle.Field(p, r, rinv, threads=16)
+    odos, _ = Fs.synth_odos(seed=41, n=3, W=20_000, fault_index=12_345)
+    # raw words may be any 128-bit value: scramble some above p
+    odos[0][0][::3, 15] = 0xEE
+    y, ff = c.recombine_verify(odos)
+    oy, off = Fs.recombine_verify(odos)
+    assert ff == off and np.array_equal(y, oy)
+    secrets = Fs.synth_words(seed=42, count=20_000, mont=False)
+    odos, _ = Fs.synth_odos(seed=43, n=2, W=20_000)
+    out, ff = c.mask_input(odos, secrets)
+    oo, off = Fs.mask_input(secrets, odos)
+    assert ff == off == -1 and np.array_equal(out, oo)
+
+
+def test_device_synth_is_honest(ctx, F, torch):
+    odos, buf, plain = ctx.synth_odos(seed=5, n=3, words=30_000, noncanon_permille=20,
+                                      with_plain=True)
+    torch.cuda.synchronize()
+    hodos = [tuple(host(f) for f in o) for o in odos]
+    oy, off = F.recombine_verify(hodos)
+    assert off == -1 and np.array_equal(oy, host(plain))
+    odos, _, _ = ctx.synth_odos(seed=5, n=2, words=30_000, fault_index=29_999)
+    _, off = F.recombine_verify([tuple(host(f) for f in o) for o in odos])
+    assert off == 29_999
+
+
+def _sample_check(F, odos_dev, y_dev, idx, host_fn):
+    sub = [tuple(host_fn(f[idx]) for f in o) for o in odos_dev]
+    oy, off = F.recombine_verify(sub)
+    assert off == -1
+    assert np.array_equal(host_fn(y_dev[idx]), oy)
+
+
+@pytest.mark.parametrize("n,W", [(2, 1 << 20), (3, 1 << 24)])
+def test_baseline_sizes(ctx, F, torch, n, W):
+    """C2 (1 Mi words, 2 parties) and C3 (16 Mi words, 3 parties) on device."""
+    odos, buf, _ = ctx.synth_odos(seed=99, n=n, words=W, noncanon_permille=5)
+    y, ff = ctx.recombine_verify(odos)
+    assert ff_dev(ff) == -1
+    idx = torch.randint(0, W, (4096,), device="cuda", generator=torch.Generator("cuda").manual_seed(1))
+    _sample_check(F, odos, y, idx, host)
+    secrets = ctx.synth_words(seed=98, count=W)
+    masked, ff = ctx.mask_input(odos, secrets)
+    assert ff_dev(ff) == -1
+    # round trip (DefaultAmphoraClientTest.java:193-235): masked + mask == secret
+    sub_o = [tuple(host(f[idx]) for f in o) for o in odos]
+    sec = host(secrets[idx])
+    oo, _ = F.mask_input(sec, sub_o)
+    assert np.array_equal(host(masked[idx]), oo)
+    del buf
+    # faulted: the kernel finds exactly the injected index
+    fault = W // 3
+    odos, buf, _ = ctx.synth_odos(seed=97, n=n, words=W, fault_index=fault)
+    _, ff = ctx.recombine_verify(odos)
+    assert ff_dev(ff) == fault
+    del buf
+    torch.cuda.empty_cache()

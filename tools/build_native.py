@@ -1,0 +1,55 @@
+"""Build libamphora_hip.so (HIP kernels + C ABI) in-tree for gfx950.
+
+    python tools/build_native.py [--force]     # or __graft_entry__.build()
+
+hipcc cross-compiles without a GPU.  The .so lands next to this file so it
+travels with the repo snapshot to the GPU box (it is git-ignored).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.join(ROOT, "amphora_amd")
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libamphora_hip.so")
+SOURCES = [os.path.join(CSRC, f) for f in ("kernels.hip", "capi.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("field.hpp", "kernels.hpp")] + [
+    os.path.join(ROOT, "include", "amphora.h")]
+ARCH = os.environ.get("AMPH_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if cand and (os.path.isabs(cand) and os.path.exists(cand) or not os.path.isabs(cand)):
+            return cand
+    return "hipcc"
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(d) <= t for d in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return LIB
+    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-mcode-object-version=5", "-Wall", "-I" + os.path.join(ROOT, "include"),
+           "-Wl,-rpath,/opt/rocm/lib", "-o", LIB + ".tmp"] + SOURCES
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("hipcc failed building libamphora_hip.so")
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))
