@@ -76,7 +76,7 @@ def cpu_baseline(n: int, budget_s: float):
     return {"value": done / el, "unit": "words/s", "cores": threads, "kind": "port",
             "sample": "%d words x %d reps (%.1f s): C oracle restating the Java BigInteger "
                       "path (maskInput+verify on %d-party mask ODOs, recombine+verify on "
-                      "share ODOs), OpenMP %d threads" % (Ws, done // Ws, el, n, n, threads)}
+                      "share ODOs), OpenMP %d threads" % (Ws, done // Ws, el, n, threads)}
 
 
 def main():
