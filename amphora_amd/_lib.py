@@ -21,6 +21,7 @@ LIB_PATH = os.path.join(HERE, "libamphora_hip.so")
 
 AMPH_OK, AMPH_E_VERIFY, AMPH_E_LEN, AMPH_E_PARAM, AMPH_E_HIP, AMPH_E_NOMEM = 0, 1, 2, 3, 4, 5
 AMPH_F_DEVICE = 1
+AMPH_F_ACCUMULATE = 2
 AMPH_NO_FAILURE = 0x7F7F7F7F7F7F7F7F
 MAX_PARTIES = 16
 
@@ -37,7 +38,7 @@ _STATUS = {AMPH_E_VERIFY: "verification failed", AMPH_E_LEN: "length invariant",
 
 def _load():
     if not os.path.exists(LIB_PATH):
-        raise ImportError("libamphora_hip.so not built (%s): run `python -m amphora_amd.build` "
+        raise ImportError("libamphora_hip.so not built (%s): run `python tools/build_native.py` "
                           "or __graft_entry__.build(); there is no CPU fallback" % LIB_PATH)
     # torch (if present) ships its own libamdhip64.so.7; loading it first makes
     # this library bind to the same HIP runtime instance (same SONAME), so

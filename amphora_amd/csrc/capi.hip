@@ -98,7 +98,8 @@ struct amph_ctx {
   u128 p = 0, r = 0, rinv = 0;
   std::mutex mu;
   size_t batch_words = (size_t)4 << 20;
-  int grid_cap = 2048;
+  int grid_cap = 0;
+  int block = 0;  // 0 = by size (block_for)
   hipStream_t streams[2] = {nullptr, nullptr};
   DevBuf slot[2];
   DevBuf ff;  // per-batch first-fail words (host path)
@@ -144,7 +145,17 @@ u128 mulmod_host(const amph_ctx* c, u128 a, u128 b) {  // a < p
   return u128_of(amph::mont_mul(amph::mont_mul(w4_of(a), w4_of(b), c->f), amph::r2_word(c->f), c->f));
 }
 
-amph::LaunchCfg cfg(amph_ctx* c, hipStream_t s) { return amph::LaunchCfg{s, c->grid_cap}; }
+// Workgroup size: 1024 threads (16 waves).  Measured through bench.py on
+// MI355X (gpurun_out r01c sweep): 1024 beat 128/256/512 by 2-5 % at both
+// 1 Mi words x 2 parties and 16 Mi words x 3 parties.  AMPH_BLOCK overrides.
+int block_for(const amph_ctx* c, size_t words) {
+  (void)words;
+  return c->block > 0 ? c->block : 1024;
+}
+
+amph::LaunchCfg cfg(amph_ctx* c, hipStream_t s, size_t words) {
+  return amph::LaunchCfg{s, c->grid_cap, block_for(c, words)};
+}
 
 // ---- host batching ------------------------------------------------------------
 // A batched host call is described by its input and output arrays, each with
@@ -202,7 +213,7 @@ int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
       cur += (cnt * o.bytes_per_word + 255) & ~(size_t)255;
     }
     unsigned long long* ff = with_ff ? (unsigned long long*)c->ff.p + b : nullptr;
-    hipError_t e = launch(din, dout, cnt, ff, cfg(c, st));
+    hipError_t e = launch(din, dout, cnt, ff, cfg(c, st, cnt));
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
     for (size_t k = 0; k < outs.size(); ++k)
       HIP_TRY(hipMemcpyAsync(outs[k].host + base * outs[k].bytes_per_word, dout[k],
@@ -250,10 +261,11 @@ const uint8_t* odo_field(const amph_odo& o, int k) {
   }
 }
 
-// device-mode first-fail: reset to the sentinel on the caller's stream
-int reset_ff_dev(int64_t* ff, hipStream_t s) {
+// device-mode first-fail: reset to the sentinel on the caller's stream,
+// unless the caller accumulates (AMPH_F_ACCUMULATE: min-combine into it)
+int reset_ff_dev(int64_t* ff, uint32_t flags, hipStream_t s) {
   if (!ff) return fail(AMPH_E_PARAM, "first_fail is required");
-  HIP_TRY(hipMemsetAsync(ff, 0x7F, sizeof(int64_t), s));
+  if (!(flags & AMPH_F_ACCUMULATE)) HIP_TRY(hipMemsetAsync(ff, 0x7F, sizeof(int64_t), s));
   return AMPH_OK;
 }
 
@@ -290,7 +302,11 @@ int amph_ctx_create(const uint8_t p_le[16], const uint8_t r_le[16], const uint8_
     return st;
   }
   c->device = device;
-  if (const char* g = std::getenv("AMPH_GRID_CAP")) c->grid_cap = std::max(1, std::atoi(g));
+  if (const char* g = std::getenv("AMPH_GRID_CAP")) c->grid_cap = std::max(0, std::atoi(g));
+  if (const char* b = std::getenv("AMPH_BLOCK")) {
+    const int v = std::atoi(b);
+    if (v >= 64 && v <= amph::kMaxBlock && v % 64 == 0) c->block = v;
+  }
   *out = c;
   return AMPH_OK;
 }
@@ -327,12 +343,12 @@ int amph_recombine_verify(amph_ctx* c, const amph_odo* odos, int n, uint8_t* out
   if (flags & AMPH_F_DEVICE) {
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipSetDevice(c->device));
-    if (int st = reset_ff_dev(first_fail, s)) return st;
+    if (int st = reset_ff_dev(first_fail, flags, s)) return st;
     amph::OdoSet set{};
     for (int k = 0; k < 5; ++k)
       for (int j = 0; j < n; ++j) set.f[k][j] = (const uint4*)odo_field(odos[j], k);
     hipError_t e = amph::launch_recombine_verify(set, n, W, (uint4*)out_secrets,
-                                                 (unsigned long long*)first_fail, c->f, cfg(c, s));
+                                                 (unsigned long long*)first_fail, c->f, cfg(c, s, W));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_rv");
   }
   std::lock_guard<std::mutex> g(c->mu);
@@ -361,13 +377,13 @@ int amph_mask_input(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* sec
   if (flags & AMPH_F_DEVICE) {
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipSetDevice(c->device));
-    if (int st = reset_ff_dev(first_fail, s)) return st;
+    if (int st = reset_ff_dev(first_fail, flags, s)) return st;
     amph::OdoSet set{};
     for (int k = 0; k < 5; ++k)
       for (int j = 0; j < n; ++j) set.f[k][j] = (const uint4*)odo_field(odos[j], k);
     hipError_t e = amph::launch_mask_input(set, n, W, (const uint4*)secrets, n_secrets,
                                            (uint4*)out_masked, (unsigned long long*)first_fail,
-                                           c->f, cfg(c, s));
+                                           c->f, cfg(c, s, W));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_mask");
   }
   std::lock_guard<std::mutex> g(c->mu);
@@ -422,7 +438,7 @@ int amph_recombine(amph_ctx* c, const uint8_t* const* shares, int n, size_t nbyt
     HIP_TRY(hipSetDevice(c->device));
     amph::ShareSet set{};
     for (int j = 0; j < n; ++j) set.s[j] = (const uint4*)shares[j];
-    hipError_t e = amph::launch_recombine(set, n, W, (uint4*)out, c->f, cfg(c, (hipStream_t)stream));
+    hipError_t e = amph::launch_recombine(set, n, W, (uint4*)out, c->f, cfg(c, (hipStream_t)stream, W));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_recombine");
   }
   std::lock_guard<std::mutex> g(c->mu);
@@ -445,10 +461,10 @@ int amph_verify(amph_ctx* c, const uint8_t* y, const uint8_t* r, const uint8_t* 
   if (flags & AMPH_F_DEVICE) {
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipSetDevice(c->device));
-    if (int st = reset_ff_dev(first_fail, s)) return st;
+    if (int st = reset_ff_dev(first_fail, flags, s)) return st;
     hipError_t e = amph::launch_verify((const uint4*)y, (const uint4*)r, (const uint4*)u,
                                        (const uint4*)v, (const uint4*)w, words,
-                                       (unsigned long long*)first_fail, c->f, cfg(c, s));
+                                       (unsigned long long*)first_fail, c->f, cfg(c, s, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_verify");
   }
   std::lock_guard<std::mutex> g(c->mu);
@@ -491,7 +507,7 @@ int amph_convert_share(amph_ctx* c, const uint8_t* masked, const uint8_t* tuples
     HIP_TRY(hipSetDevice(c->device));
     hipError_t e = amph::launch_convert_share((const uint4*)masked, (const uint4*)tuples, words,
                                               alpha, use_zero, (uint4*)out, c->f,
-                                              cfg(c, (hipStream_t)stream));
+                                              cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_conv");
   }
   std::lock_guard<std::mutex> g(c->mu);
@@ -518,7 +534,7 @@ int amph_odo_pre(amph_ctx* c, const uint8_t* share_data, size_t share_stride,
     hipError_t e = amph::launch_odo_pre((const uint4*)share_data, sw, (const uint4*)masks,
                                         (const uint4*)triples, words, (uint4*)oy, (uint4*)orr,
                                         (uint4*)ov, (uint4*)omag, (uint32_t*)oneg, c->f,
-                                        cfg(c, (hipStream_t)stream));
+                                        cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_odo_pre");
   }
   std::lock_guard<std::mutex> g(c->mu);
@@ -548,7 +564,7 @@ int amph_open_diffs(amph_ctx* c, const uint8_t* const* mags, const uint8_t* cons
       set.mag[j] = (const uint4*)mags[j];
       set.neg[j] = (const uint32_t*)negs[j];
     }
-    hipError_t e = amph::launch_open_diffs(set, n, W, (uint4*)out, c->f, cfg(c, (hipStream_t)stream));
+    hipError_t e = amph::launch_open_diffs(set, n, W, (uint4*)out, c->f, cfg(c, (hipStream_t)stream, W));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_open");
   }
   std::lock_guard<std::mutex> g(c->mu);
@@ -575,7 +591,7 @@ int amph_odo_post(amph_ctx* c, const uint8_t* opened, const uint8_t* triples, si
     HIP_TRY(hipSetDevice(c->device));
     hipError_t e = amph::launch_odo_post((const uint4*)opened, (const uint4*)triples, words,
                                          is_player0, (uint4*)ow, (uint4*)ou, c->f,
-                                         cfg(c, (hipStream_t)stream));
+                                         cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_odo_post");
   }
   std::lock_guard<std::mutex> g(c->mu);
@@ -594,7 +610,7 @@ int amph_to_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, uint
   if (words && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     HIP_TRY(hipSetDevice(c->device));
-    hipError_t e = amph::launch_to_gfp((const uint4*)in, words, (uint4*)out, c->f, cfg(c, (hipStream_t)stream));
+    hipError_t e = amph::launch_to_gfp((const uint4*)in, words, (uint4*)out, c->f, cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_to_gfp");
   }
   std::lock_guard<std::mutex> g(c->mu);
@@ -611,7 +627,7 @@ int amph_from_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, ui
   if (words && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     HIP_TRY(hipSetDevice(c->device));
-    hipError_t e = amph::launch_from_gfp((const uint4*)in, words, (uint4*)out, c->f, cfg(c, (hipStream_t)stream));
+    hipError_t e = amph::launch_from_gfp((const uint4*)in, words, (uint4*)out, c->f, cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_from_gfp");
   }
   std::lock_guard<std::mutex> g(c->mu);
@@ -629,7 +645,7 @@ int amph_mask_words(amph_ctx* c, const uint8_t* secrets, const uint8_t* masks, s
   if (flags & AMPH_F_DEVICE) {
     HIP_TRY(hipSetDevice(c->device));
     hipError_t e = amph::launch_mask_words((const uint4*)secrets, (const uint4*)masks, words,
-                                           (uint4*)out, c->f, cfg(c, (hipStream_t)stream));
+                                           (uint4*)out, c->f, cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_mask_words");
   }
   std::lock_guard<std::mutex> g(c->mu);
@@ -653,7 +669,7 @@ int amph_synth_odos(amph_ctx* c, uint64_t seed, int n, size_t words, uint8_t* co
     }
   HIP_TRY(hipSetDevice(c->device));
   hipError_t e = amph::launch_synth_odos(set, n, words, seed, (uint4*)out_plain_y, fault_index,
-                                         noncanon_permille, c->f, cfg(c, (hipStream_t)stream));
+                                         noncanon_permille, c->f, cfg(c, (hipStream_t)stream, words));
   return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_synth");
 }
 
@@ -661,7 +677,7 @@ int amph_synth_words(amph_ctx* c, uint64_t seed, size_t count, uint8_t* out, voi
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (count && !out) return fail(AMPH_E_PARAM, "null output");
   HIP_TRY(hipSetDevice(c->device));
-  hipError_t e = amph::launch_synth_words((uint4*)out, count, seed, c->f, cfg(c, (hipStream_t)stream));
+  hipError_t e = amph::launch_synth_words((uint4*)out, count, seed, c->f, cfg(c, (hipStream_t)stream, count));
   return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_synth_words");
 }
 

@@ -81,10 +81,10 @@ __device__ __forceinline__ void recombine5(const OdoSet& odo, int n, size_t i, c
 }
 
 template <int NP, bool BIG>
-__global__ __launch_bounds__(kBlock) void k_rv(OdoSet odo, int n, size_t words, uint4* out_y,
+__global__ __launch_bounds__(kMaxBlock) void k_rv(OdoSet odo, int n, size_t words, uint4* out_y,
                                               unsigned long long* ff, Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += stride) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
     W4 a[5];
     recombine5<NP, BIG>(odo, n, i, f, a);
     const bool ok = (int)eq(mont_mul(a[0], a[1], f), a[3]) & (int)eq(mont_mul(a[2], a[1], f), a[4]);
@@ -94,12 +94,12 @@ __global__ __launch_bounds__(kBlock) void k_rv(OdoSet odo, int n, size_t words, 
 }
 
 template <int NP, bool BIG>
-__global__ __launch_bounds__(kBlock) void k_mask(OdoSet odo, int n, size_t words,
+__global__ __launch_bounds__(kMaxBlock) void k_mask(OdoSet odo, int n, size_t words,
                                                 const uint4* secrets, size_t n_secrets,
                                                 uint4* out, unsigned long long* ff, Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
   const W4 r2 = r2_word(f);
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += stride) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
     const bool has_secret = i < n_secrets;
     const uint4 s = has_secret ? ld(secrets + i) : make_uint4(0, 0, 0, 0);
     W4 a[5];
@@ -111,19 +111,19 @@ __global__ __launch_bounds__(kBlock) void k_mask(OdoSet odo, int n, size_t words
 }
 
 template <int NP, bool BIG>
-__global__ __launch_bounds__(kBlock) void k_recombine(ShareSet sh, int n, size_t words,
+__global__ __launch_bounds__(kMaxBlock) void k_recombine(ShareSet sh, int n, size_t words,
                                                      uint4* out, Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += stride)
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride)
     st(out + i, redc(sum_field<NP, BIG>(sh.s, n, i, f), f));
 }
 
 template <bool BIG>
-__global__ __launch_bounds__(kBlock) void k_verify(const uint4* y, const uint4* r, const uint4* u,
+__global__ __launch_bounds__(kMaxBlock) void k_verify(const uint4* y, const uint4* r, const uint4* u,
                                                   const uint4* v, const uint4* w, size_t words,
                                                   unsigned long long* ff, Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += stride) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
     const W4 Y = canon<BIG>(w4(ld(y + i)), f), R = canon<BIG>(w4(ld(r + i)), f);
     const W4 V = canon<BIG>(w4(ld(v + i)), f);
     const W4 Wd = w4(ld(w + i)), Ud = w4(ld(u + i));
@@ -134,11 +134,11 @@ __global__ __launch_bounds__(kBlock) void k_verify(const uint4* y, const uint4* 
 }
 
 template <bool BIG>
-__global__ __launch_bounds__(kBlock) void k_conv(const uint4* masked, const uint4* tuples,
+__global__ __launch_bounds__(kMaxBlock) void k_conv(const uint4* masked, const uint4* tuples,
                                                 size_t words, W4 alpha, int use_zero,
                                                 uint4* out, Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += stride) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
     const uint4 mr = ld(masked + i), vr = ld(tuples + 2 * i), cr = ld(tuples + 2 * i + 1);
     const W4 m = canon<BIG>(w4(mr), f);
     const W4 val = canon<BIG>(w4(vr), f), mac = canon<BIG>(w4(cr), f);
@@ -156,12 +156,12 @@ __device__ __forceinline__ uint32_t signed_diff(const W4& x, const W4& a, W4& ma
   return neg;
 }
 
-__global__ __launch_bounds__(kBlock) void k_odo_pre(const uint4* share_data, int stride_w,
+__global__ __launch_bounds__(kMaxBlock) void k_odo_pre(const uint4* share_data, int stride_w,
                                                    const uint4* masks, const uint4* triples,
                                                    size_t words, uint4* oy, uint4* orr, uint4* ov,
                                                    uint4* omag, uint32_t* oneg, Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += stride) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
     const uint4 yr = ld(share_data + (size_t)stride_w * i);
     const uint4 m1 = ld(masks + 4 * i), m2 = ld(masks + 4 * i + 2);
     const uint4* t0 = triples + 12 * i;  // triple 2i: a = t0[0], b = t0[2]
@@ -184,11 +184,11 @@ __global__ __launch_bounds__(kBlock) void k_odo_pre(const uint4* share_data, int
 }
 
 template <int NP, bool BIG>
-__global__ __launch_bounds__(kBlock) void k_open(SignedSet d, int n, size_t words, uint4* out,
+__global__ __launch_bounds__(kMaxBlock) void k_open(SignedSet d, int n, size_t words, uint4* out,
                                                 Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
   const int np = NP > 0 ? NP : n;
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += stride) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
     W4 acc[4] = {};
     for (int j = 0; j < np; ++j) {
       const uint32_t s = d.neg[j][i];
@@ -204,12 +204,12 @@ __global__ __launch_bounds__(kBlock) void k_open(SignedSet d, int n, size_t word
 }
 
 template <bool BIG>
-__global__ __launch_bounds__(kBlock) void k_odo_post(const uint4* opened, const uint4* triples,
+__global__ __launch_bounds__(kMaxBlock) void k_odo_post(const uint4* opened, const uint4* triples,
                                                     size_t words, int p0, uint4* ow, uint4* ou,
                                                     Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
   const W4 r2 = r2_word(f);
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += stride) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
     W4 z[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -230,25 +230,25 @@ __global__ __launch_bounds__(kBlock) void k_odo_post(const uint4* opened, const 
 // MpSpdzIntegrationUtils.toGfp / fromGfp over arrays, and maskInput with
 // canonical masks (SecretShareUtil.java:65-68 word by word).
 template <bool BIG>
-__global__ __launch_bounds__(kBlock) void k_to_gfp(const uint4* in, size_t words, uint4* out, Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
+__global__ __launch_bounds__(kMaxBlock) void k_to_gfp(const uint4* in, size_t words, uint4* out, Fp f) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
   const W4 r2 = r2_word(f);
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += stride)
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride)
     st(out + i, mont_mul(w4(ld(in + i)), r2, f));
 }
 
-__global__ __launch_bounds__(kBlock) void k_from_gfp(const uint4* in, size_t words, uint4* out, Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += stride)
+__global__ __launch_bounds__(kMaxBlock) void k_from_gfp(const uint4* in, size_t words, uint4* out, Fp f) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride)
     st(out + i, redc(w4(ld(in + i)), f));
 }
 
 template <bool BIG>
-__global__ __launch_bounds__(kBlock) void k_mask_words(const uint4* secrets, const uint4* masks,
+__global__ __launch_bounds__(kMaxBlock) void k_mask_words(const uint4* secrets, const uint4* masks,
                                                       size_t words, uint4* out, Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
   const W4 r2 = r2_word(f);
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += stride) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
     const W4 s = mont_mul(w4(ld(secrets + i)), r2, f), m = mont_mul(w4(ld(masks + i)), r2, f);
     st(out + i, mod_sub(s, m, f));
   }
@@ -269,12 +269,12 @@ __device__ __forceinline__ W4 rand_fe(uint64_t seed, uint64_t ctr, const Fp& f) 
 }
 
 template <bool BIG>
-__global__ __launch_bounds__(kBlock) void k_synth(OutSet out, int n, size_t words, uint64_t seed,
+__global__ __launch_bounds__(kMaxBlock) void k_synth(OutSet out, int n, size_t words, uint64_t seed,
                                                  uint4* plain_y, long long fault, int permille,
                                                  Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
   const W4 one = redc(r2_word(f), f);  // [1] = R mod p
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += stride) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
     const uint64_t base = (uint64_t)i * 64;
     W4 val[5];
     val[0] = rand_fe<BIG>(seed, base + 0, f);
@@ -313,17 +313,20 @@ __global__ __launch_bounds__(kBlock) void k_synth(OutSet out, int n, size_t word
 }
 
 template <bool BIG>
-__global__ __launch_bounds__(kBlock) void k_synth_words(uint4* out, size_t count, uint64_t seed,
+__global__ __launch_bounds__(kMaxBlock) void k_synth_words(uint4* out, size_t count, uint64_t seed,
                                                        Fp f) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < count; i += stride)
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride)
     st(out + i, rand_fe<BIG>(seed, i, f));
 }
 
+// One word per thread over a full grid: measured faster than a capped
+// grid-stride loop (tools/ubench: 1.1-1.15x at 1-16 Mi words).  grid_cap > 0
+// caps the grid (the kernels grid-stride past it).
 unsigned grid_for(size_t words, const LaunchCfg& c) {
-  size_t g = (words + kBlock - 1) / kBlock;
-  const size_t cap = c.grid_cap > 0 ? (size_t)c.grid_cap : 2048;
-  if (g > cap) g = cap;
+  size_t g = (words + c.block - 1) / c.block;
+  if (c.grid_cap > 0 && g > (size_t)c.grid_cap) g = (size_t)c.grid_cap;
+  if (g > 0x7FFFFFFFu) g = 0x7FFFFFFFu;
   if (g == 0) g = 1;
   return (unsigned)g;
 }
@@ -345,7 +348,7 @@ hipError_t launch_recombine_verify(const OdoSet& odo, int n, size_t words, uint4
                                    unsigned long long* ff, const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-#define L(NP, BIG) hipLaunchKernelGGL((k_rv<NP, BIG>), dim3(g), dim3(kBlock), 0, c.stream, odo, n, words, out_y, ff, f)
+#define L(NP, BIG) hipLaunchKernelGGL((k_rv<NP, BIG>), dim3(g), dim3(c.block), 0, c.stream, odo, n, words, out_y, ff, f)
   if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
   return hipGetLastError();
@@ -356,7 +359,7 @@ hipError_t launch_mask_input(const OdoSet& odo, int n, size_t words, const uint4
                              const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-#define L(NP, BIG) hipLaunchKernelGGL((k_mask<NP, BIG>), dim3(g), dim3(kBlock), 0, c.stream, odo, n, words, secrets, n_secrets, out, ff, f)
+#define L(NP, BIG) hipLaunchKernelGGL((k_mask<NP, BIG>), dim3(g), dim3(c.block), 0, c.stream, odo, n, words, secrets, n_secrets, out, ff, f)
   if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
   return hipGetLastError();
@@ -366,7 +369,7 @@ hipError_t launch_recombine(const ShareSet& sh, int n, size_t words, uint4* out,
                             const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-#define L(NP, BIG) hipLaunchKernelGGL((k_recombine<NP, BIG>), dim3(g), dim3(kBlock), 0, c.stream, sh, n, words, out, f)
+#define L(NP, BIG) hipLaunchKernelGGL((k_recombine<NP, BIG>), dim3(g), dim3(c.block), 0, c.stream, sh, n, words, out, f)
   if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
   return hipGetLastError();
@@ -377,8 +380,8 @@ hipError_t launch_verify(const uint4* y, const uint4* r, const uint4* u, const u
                          const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-  if (f.big) hipLaunchKernelGGL((k_verify<true>), dim3(g), dim3(kBlock), 0, c.stream, y, r, u, v, w, words, ff, f);
-  else hipLaunchKernelGGL((k_verify<false>), dim3(g), dim3(kBlock), 0, c.stream, y, r, u, v, w, words, ff, f);
+  if (f.big) hipLaunchKernelGGL((k_verify<true>), dim3(g), dim3(c.block), 0, c.stream, y, r, u, v, w, words, ff, f);
+  else hipLaunchKernelGGL((k_verify<false>), dim3(g), dim3(c.block), 0, c.stream, y, r, u, v, w, words, ff, f);
   return hipGetLastError();
 }
 
@@ -386,8 +389,8 @@ hipError_t launch_convert_share(const uint4* masked, const uint4* tuples, size_t
                                 int use_zero, uint4* out, const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-  if (f.big) hipLaunchKernelGGL((k_conv<true>), dim3(g), dim3(kBlock), 0, c.stream, masked, tuples, words, alpha, use_zero, out, f);
-  else hipLaunchKernelGGL((k_conv<false>), dim3(g), dim3(kBlock), 0, c.stream, masked, tuples, words, alpha, use_zero, out, f);
+  if (f.big) hipLaunchKernelGGL((k_conv<true>), dim3(g), dim3(c.block), 0, c.stream, masked, tuples, words, alpha, use_zero, out, f);
+  else hipLaunchKernelGGL((k_conv<false>), dim3(g), dim3(c.block), 0, c.stream, masked, tuples, words, alpha, use_zero, out, f);
   return hipGetLastError();
 }
 
@@ -395,7 +398,7 @@ hipError_t launch_odo_pre(const uint4* share_data, int stride_w, const uint4* ma
                           const uint4* triples, size_t words, uint4* oy, uint4* orr, uint4* ov,
                           uint4* omag, uint32_t* oneg, const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_odo_pre, dim3(grid_for(words, c)), dim3(kBlock), 0, c.stream, share_data,
+  hipLaunchKernelGGL(k_odo_pre, dim3(grid_for(words, c)), dim3(c.block), 0, c.stream, share_data,
                      stride_w, masks, triples, words, oy, orr, ov, omag, oneg, f);
   return hipGetLastError();
 }
@@ -404,7 +407,7 @@ hipError_t launch_open_diffs(const SignedSet& d, int n, size_t words, uint4* out
                              const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-#define L(NP, BIG) hipLaunchKernelGGL((k_open<NP, BIG>), dim3(g), dim3(kBlock), 0, c.stream, d, n, words, out, f)
+#define L(NP, BIG) hipLaunchKernelGGL((k_open<NP, BIG>), dim3(g), dim3(c.block), 0, c.stream, d, n, words, out, f)
   if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
   return hipGetLastError();
@@ -414,8 +417,8 @@ hipError_t launch_odo_post(const uint4* opened, const uint4* triples, size_t wor
                            uint4* ow, uint4* ou, const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-  if (f.big) hipLaunchKernelGGL((k_odo_post<true>), dim3(g), dim3(kBlock), 0, c.stream, opened, triples, words, p0, ow, ou, f);
-  else hipLaunchKernelGGL((k_odo_post<false>), dim3(g), dim3(kBlock), 0, c.stream, opened, triples, words, p0, ow, ou, f);
+  if (f.big) hipLaunchKernelGGL((k_odo_post<true>), dim3(g), dim3(c.block), 0, c.stream, opened, triples, words, p0, ow, ou, f);
+  else hipLaunchKernelGGL((k_odo_post<false>), dim3(g), dim3(c.block), 0, c.stream, opened, triples, words, p0, ow, ou, f);
   return hipGetLastError();
 }
 
@@ -423,15 +426,15 @@ hipError_t launch_to_gfp(const uint4* in, size_t words, uint4* out, const Fp& f,
                          const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-  if (f.big) hipLaunchKernelGGL((k_to_gfp<true>), dim3(g), dim3(kBlock), 0, c.stream, in, words, out, f);
-  else hipLaunchKernelGGL((k_to_gfp<false>), dim3(g), dim3(kBlock), 0, c.stream, in, words, out, f);
+  if (f.big) hipLaunchKernelGGL((k_to_gfp<true>), dim3(g), dim3(c.block), 0, c.stream, in, words, out, f);
+  else hipLaunchKernelGGL((k_to_gfp<false>), dim3(g), dim3(c.block), 0, c.stream, in, words, out, f);
   return hipGetLastError();
 }
 
 hipError_t launch_from_gfp(const uint4* in, size_t words, uint4* out, const Fp& f,
                            const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_from_gfp, dim3(grid_for(words, c)), dim3(kBlock), 0, c.stream, in, words, out, f);
+  hipLaunchKernelGGL(k_from_gfp, dim3(grid_for(words, c)), dim3(c.block), 0, c.stream, in, words, out, f);
   return hipGetLastError();
 }
 
@@ -439,8 +442,8 @@ hipError_t launch_mask_words(const uint4* secrets, const uint4* masks, size_t wo
                              const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-  if (f.big) hipLaunchKernelGGL((k_mask_words<true>), dim3(g), dim3(kBlock), 0, c.stream, secrets, masks, words, out, f);
-  else hipLaunchKernelGGL((k_mask_words<false>), dim3(g), dim3(kBlock), 0, c.stream, secrets, masks, words, out, f);
+  if (f.big) hipLaunchKernelGGL((k_mask_words<true>), dim3(g), dim3(c.block), 0, c.stream, secrets, masks, words, out, f);
+  else hipLaunchKernelGGL((k_mask_words<false>), dim3(g), dim3(c.block), 0, c.stream, secrets, masks, words, out, f);
   return hipGetLastError();
 }
 
@@ -449,8 +452,8 @@ hipError_t launch_synth_odos(const OutSet& out, int n, size_t words, uint64_t se
                              const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-  if (f.big) hipLaunchKernelGGL((k_synth<true>), dim3(g), dim3(kBlock), 0, c.stream, out, n, words, seed, plain_y, fault, permille, f);
-  else hipLaunchKernelGGL((k_synth<false>), dim3(g), dim3(kBlock), 0, c.stream, out, n, words, seed, plain_y, fault, permille, f);
+  if (f.big) hipLaunchKernelGGL((k_synth<true>), dim3(g), dim3(c.block), 0, c.stream, out, n, words, seed, plain_y, fault, permille, f);
+  else hipLaunchKernelGGL((k_synth<false>), dim3(g), dim3(c.block), 0, c.stream, out, n, words, seed, plain_y, fault, permille, f);
   return hipGetLastError();
 }
 
@@ -458,8 +461,8 @@ hipError_t launch_synth_words(uint4* out, size_t count, uint64_t seed, const Fp&
                               const LaunchCfg& c) {
   if (count == 0) return hipSuccess;
   const unsigned g = grid_for(count, c);
-  if (f.big) hipLaunchKernelGGL((k_synth_words<true>), dim3(g), dim3(kBlock), 0, c.stream, out, count, seed, f);
-  else hipLaunchKernelGGL((k_synth_words<false>), dim3(g), dim3(kBlock), 0, c.stream, out, count, seed, f);
+  if (f.big) hipLaunchKernelGGL((k_synth_words<true>), dim3(g), dim3(c.block), 0, c.stream, out, count, seed, f);
+  else hipLaunchKernelGGL((k_synth_words<false>), dim3(g), dim3(c.block), 0, c.stream, out, count, seed, f);
   return hipGetLastError();
 }
 

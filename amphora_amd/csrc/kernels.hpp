@@ -9,7 +9,7 @@
 namespace amph {
 
 constexpr int kMaxParties = 16;
-constexpr int kBlock = 256;
+constexpr int kMaxBlock = 1024;  // kernels accept any block size <= this
 // first_fail sentinel: what hipMemsetAsync(.., 0x7F, 8) leaves behind.
 constexpr unsigned long long kNoFail = 0x7F7F7F7F7F7F7F7FULL;
 
@@ -30,7 +30,8 @@ struct SignedSet {  // per party: diff magnitudes (2 words per pair) + sign word
 
 struct LaunchCfg {
   hipStream_t stream;
-  int grid_cap;  // max workgroups (grid-stride beyond)
+  int grid_cap;  // 0 = full grid (one word per thread); > 0 caps it (grid-stride beyond)
+  int block;     // threads per workgroup, multiple of 64, <= kMaxBlock
 };
 
 // K_RV: recombine 5 fields over n parties, verify w == y r, u == v r,

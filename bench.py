@@ -101,7 +101,10 @@ def main():
     secrets = ctx.synth_words(seed=3000 + rank, count=W)
     torch.cuda.synchronize()
 
-    ff = torch.empty(2, dtype=torch.int64, device="cuda")
+    # first-fail words: set to the sentinel once; every step min-combines into
+    # them (AMPH_F_ACCUMULATE), so any failing word in any step stays visible
+    ff = torch.full((2,), NO_FAIL, dtype=torch.int64, device="cuda")
+    flags = A._lib.AMPH_F_DEVICE | A._lib.AMPH_F_ACCUMULATE
     lib = A._lib
     mask_arr, mviews = ctx._odo_structs(mask_odos)
     share_arr, sviews = ctx._odo_structs(share_odos)
@@ -114,12 +117,11 @@ def main():
 
     def k_mask():
         st = lib.lib.amph_mask_input(ctx._h, mask_arr, n, secrets.data_ptr(), W, masked.data_ptr(),
-                                     ff0, lib.AMPH_F_DEVICE, stream)
+                                     ff0, flags, stream)
         assert st == 0
 
     def k_rv():
-        st = lib.lib.amph_recombine_verify(ctx._h, share_arr, n, ys.data_ptr(), ff1,
-                                           lib.AMPH_F_DEVICE, stream)
+        st = lib.lib.amph_recombine_verify(ctx._h, share_arr, n, ys.data_ptr(), ff1, flags, stream)
         assert st == 0
 
     verdict = torch.empty(1, dtype=torch.int64, device="cuda")

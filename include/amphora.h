@@ -77,6 +77,11 @@ extern "C" {
 
 /* flags */
 #define AMPH_F_DEVICE 0x1u /* all buffers are device pointers; async on `stream` */
+/* with AMPH_F_DEVICE: do not reset *first_fail before the launch; the kernel
+ * min-combines its failing index (local to this call) into the value there.
+ * The caller sets it to AMPH_NO_FAILURE once before a run of calls (saves
+ * one memset launch per call; used by bench.py and for repeated passes). */
+#define AMPH_F_ACCUMULATE 0x2u
 
 /* value of a device-side first_fail word when every word verified */
 #define AMPH_NO_FAILURE ((int64_t)0x7F7F7F7F7F7F7F7FLL)
