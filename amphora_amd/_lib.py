@@ -70,6 +70,8 @@ def _load():
     L.amph_odo_pre.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp, u32, vp]
     L.amph_open_diffs.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), i32, sz, vp, u32, vp]
     L.amph_odo_post.argtypes = [vp, vp, vp, sz, i32, vp, vp, u32, vp]
+    L.amph_host_register.argtypes = [vp, vp, sz]
+    L.amph_host_unregister.argtypes = [vp, vp]
     L.amph_synth_odos.argtypes = [vp, u64, i32, sz, C.POINTER(vp), vp, C.c_int64, i32, vp]
     L.amph_synth_words.argtypes = [vp, u64, sz, vp, vp]
     return L
@@ -82,7 +84,7 @@ EXPORTED = ["amph_ctx_create", "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_
             "amph_mask_input", "amph_recombine", "amph_verify", "amph_verify_message",
             "amph_mask_words", "amph_to_gfp", "amph_from_gfp", "amph_convert_share",
             "amph_odo_pre", "amph_open_diffs", "amph_odo_post", "amph_synth_odos",
-            "amph_synth_words"]
+            "amph_synth_words", "amph_host_register", "amph_host_unregister"]
 
 
 class _AmphOdo(C.Structure):
@@ -142,6 +144,13 @@ class Context:
 
     def set_batch_words(self, words: int):
         self._check(lib.amph_ctx_set_batch_words(self._h, words))
+
+    def host_register(self, array: np.ndarray):
+        """Page-lock a numpy buffer so host-pointer calls DMA it directly."""
+        self._check(lib.amph_host_register(self._h, array.ctypes.data, array.nbytes))
+
+    def host_unregister(self, array: np.ndarray):
+        self._check(lib.amph_host_unregister(self._h, array.ctypes.data))
 
     # -- mode plumbing ----------------------------------------------------------
     def _mode(self, *arrays):

@@ -16,7 +16,11 @@
 #include <string>
 #include <vector>
 
+#include <memory>
+#include <thread>
+
 #include "../../include/amphora.h"
+#include "host_stream.hpp"
 #include "kernels.hpp"
 
 using amph::Fp;
@@ -100,9 +104,19 @@ struct amph_ctx {
   size_t batch_words = (size_t)4 << 20;
   int grid_cap = 0;
   int block = 0;  // 0 = by size (block_for)
-  hipStream_t streams[2] = {nullptr, nullptr};
-  DevBuf slot[2];
+  // host-pointer path: kSlots batches in flight, one stream each
+  static constexpr int kSlots = 3;
+  struct Slot {
+    DevBuf dev;
+    amph::PinnedBuf hin, hout;
+    hipEvent_t done = nullptr;
+    bool busy = false;
+    size_t base = 0, cnt = 0;
+  };
+  hipStream_t streams[kSlots] = {};
+  Slot slots[kSlots];
   DevBuf ff;  // per-batch first-fail words (host path)
+  std::unique_ptr<amph::CopyPool> pool;
 };
 
 namespace {
@@ -170,23 +184,55 @@ struct HostOut {
   size_t bytes_per_word;
 };
 
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int host_threads() {
+  if (const char* t = std::getenv("AMPH_HOST_THREADS")) return std::max(1, std::atoi(t));
+  const unsigned hw = std::thread::hardware_concurrency();
+  return (int)std::max(1u, std::min(8u, hw ? hw / 2 : 1u));
+}
+
+// Streams `words` through the device in batches of ctx->batch_words:
+//   stage inputs (CPU threads: pageable -> page-locked slot), HtoD, kernel,
+//   DtoH (-> page-locked slot), and copy outputs back once the slot's event
+//   fires.  kSlots batches are in flight on kSlots streams, so the HtoD of
+//   batch b+1, the kernel of batch b and the DtoH of batch b-1 overlap while
+//   the CPU stages the next batch.  Page-locked caller buffers are DMA'd
+//   directly.  Verify failures land in one device word per batch; the
+//   smallest global index is reported.
 template <class Launch>
 int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
                 const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
                 Launch&& launch) {
   if (first_fail) *first_fail = -1;
   if (words == 0) return AMPH_OK;
+  constexpr int S = amph_ctx::kSlots;
   HIP_TRY(hipSetDevice(c->device));
-  for (int s = 0; s < 2; ++s)
+  for (int s = 0; s < S; ++s) {
     if (!c->streams[s]) HIP_TRY(hipStreamCreateWithFlags(&c->streams[s], hipStreamNonBlocking));
+    if (!c->slots[s].done) HIP_TRY(hipEventCreateWithFlags(&c->slots[s].done, hipEventDisableTiming));
+    c->slots[s].busy = false;
+  }
+  if (!c->pool) c->pool.reset(new amph::CopyPool(host_threads() - 1));
   const size_t bw = std::min(words, c->batch_words);
   const size_t nb = (words + bw - 1) / bw;
-  size_t per_word = 0;
-  for (auto& i : ins) per_word += i.bytes_per_word;
-  for (auto& o : outs) per_word += o.bytes_per_word;
-  for (int s = 0; s < 2; ++s) {
-    hipError_t e = c->slot[s].ensure(per_word * bw + 256 * (ins.size() + outs.size()));
-    if (e != hipSuccess) return fail(AMPH_E_NOMEM, std::string("device scratch: ") + hipGetErrorString(e));
+  std::vector<char> in_pinned(ins.size()), out_pinned(outs.size());
+  size_t dev_bytes = 0, hin_bytes = 0, hout_bytes = 0;
+  for (size_t k = 0; k < ins.size(); ++k) {
+    in_pinned[k] = amph::is_pinned_host(ins[k].host);
+    dev_bytes += align256(bw * ins[k].bytes_per_word);
+    if (!in_pinned[k]) hin_bytes += align256(bw * ins[k].bytes_per_word);
+  }
+  for (size_t k = 0; k < outs.size(); ++k) {
+    out_pinned[k] = amph::is_pinned_host(outs[k].host);
+    dev_bytes += align256(bw * outs[k].bytes_per_word);
+    if (!out_pinned[k]) hout_bytes += align256(bw * outs[k].bytes_per_word);
+  }
+  for (int s = 0; s < S && (size_t)s < nb; ++s) {
+    hipError_t e = c->slots[s].dev.ensure(dev_bytes);
+    if (e == hipSuccess) e = c->slots[s].hin.ensure(hin_bytes);
+    if (e == hipSuccess) e = c->slots[s].hout.ensure(hout_bytes);
+    if (e != hipSuccess) return fail(AMPH_E_NOMEM, std::string("batch buffers: ") + hipGetErrorString(e));
   }
   if (with_ff) {
     hipError_t e = c->ff.ensure(nb * sizeof(unsigned long long));
@@ -194,33 +240,73 @@ int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
     HIP_TRY(hipMemsetAsync(c->ff.p, 0x7F, nb * sizeof(unsigned long long), c->streams[0]));
     HIP_TRY(hipStreamSynchronize(c->streams[0]));
   }
+  auto drain = [&](amph_ctx::Slot& sl) -> int {
+    if (!sl.busy) return AMPH_OK;
+    HIP_TRY(hipEventSynchronize(sl.done));
+    std::vector<amph::CopyTask> tasks;
+    size_t off = 0;
+    for (size_t k = 0; k < outs.size(); ++k) {
+      if (out_pinned[k]) continue;
+      tasks.push_back({outs[k].host + sl.base * outs[k].bytes_per_word, (char*)sl.hout.p + off,
+                       sl.cnt * outs[k].bytes_per_word});
+      off += align256(bw * outs[k].bytes_per_word);
+    }
+    c->pool->copy(tasks);
+    sl.busy = false;
+    return AMPH_OK;
+  };
   for (size_t b = 0; b < nb; ++b) {
-    const int s = (int)(b & 1);
-    hipStream_t st = c->streams[s];
+    amph_ctx::Slot& sl = c->slots[b % S];
+    hipStream_t st = c->streams[b % S];
+    if (int rc = drain(sl)) return rc;
     const size_t base = b * bw, cnt = std::min(bw, words - base);
-    // carve the slot: inputs then outputs, 256-B aligned
-    uint8_t* cur = (uint8_t*)c->slot[s].p;
+    // stage pageable inputs into the slot's page-locked buffer
+    std::vector<amph::CopyTask> tasks;
+    std::vector<const void*> src(ins.size());
+    size_t hoff = 0;
+    for (size_t k = 0; k < ins.size(); ++k) {
+      const uint8_t* u = ins[k].host + base * ins[k].bytes_per_word;
+      if (in_pinned[k]) {
+        src[k] = u;
+      } else {
+        void* d = (char*)sl.hin.p + hoff;
+        tasks.push_back({d, u, cnt * ins[k].bytes_per_word});
+        src[k] = d;
+        hoff += align256(bw * ins[k].bytes_per_word);
+      }
+    }
+    c->pool->copy(tasks);
+    uint8_t* cur = (uint8_t*)sl.dev.p;
     std::vector<const uint4*> din;
     std::vector<uint4*> dout;
-    for (auto& i : ins) {
-      HIP_TRY(hipMemcpyAsync(cur, i.host + base * i.bytes_per_word, cnt * i.bytes_per_word,
-                             hipMemcpyHostToDevice, st));
+    for (size_t k = 0; k < ins.size(); ++k) {
+      HIP_TRY(hipMemcpyAsync(cur, src[k], cnt * ins[k].bytes_per_word, hipMemcpyHostToDevice, st));
       din.push_back((const uint4*)cur);
-      cur += (cnt * i.bytes_per_word + 255) & ~(size_t)255;
+      cur += align256(bw * ins[k].bytes_per_word);
     }
-    for (auto& o : outs) {
+    for (size_t k = 0; k < outs.size(); ++k) {
       dout.push_back((uint4*)cur);
-      cur += (cnt * o.bytes_per_word + 255) & ~(size_t)255;
+      cur += align256(bw * outs[k].bytes_per_word);
     }
     unsigned long long* ff = with_ff ? (unsigned long long*)c->ff.p + b : nullptr;
     hipError_t e = launch(din, dout, cnt, ff, cfg(c, st, cnt));
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
-    for (size_t k = 0; k < outs.size(); ++k)
-      HIP_TRY(hipMemcpyAsync(outs[k].host + base * outs[k].bytes_per_word, dout[k],
-                             cnt * outs[k].bytes_per_word, hipMemcpyDeviceToHost, st));
+    size_t ooff = 0;
+    for (size_t k = 0; k < outs.size(); ++k) {
+      void* dst = outs[k].host + base * outs[k].bytes_per_word;
+      if (!out_pinned[k]) {
+        dst = (char*)sl.hout.p + ooff;
+        ooff += align256(bw * outs[k].bytes_per_word);
+      }
+      HIP_TRY(hipMemcpyAsync(dst, dout[k], cnt * outs[k].bytes_per_word, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipEventRecord(sl.done, st));
+    sl.busy = true;
+    sl.base = base;
+    sl.cnt = cnt;
   }
-  HIP_TRY(hipStreamSynchronize(c->streams[0]));
-  HIP_TRY(hipStreamSynchronize(c->streams[1]));
+  for (size_t b = nb > (size_t)S ? nb - S : 0; b < nb; ++b)
+    if (int rc = drain(c->slots[b % S])) return rc;
   if (with_ff) {
     std::vector<unsigned long long> h(nb);
     HIP_TRY(hipMemcpy(h.data(), c->ff.p, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -313,11 +399,14 @@ int amph_ctx_create(const uint8_t p_le[16], const uint8_t r_le[16], const uint8_
 
 void amph_ctx_destroy(amph_ctx* c) {
   if (!c) return;
-  if (c->streams[0] || c->slot[0].p || c->ff.p) {
+  if (c->streams[0] || c->slots[0].dev.p || c->ff.p) {
     (void)hipSetDevice(c->device);
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < amph_ctx::kSlots; ++s) {
       if (c->streams[s]) (void)hipStreamSynchronize(c->streams[s]);
-      c->slot[s].release();
+      c->slots[s].dev.release();
+      c->slots[s].hin.release();
+      c->slots[s].hout.release();
+      if (c->slots[s].done) (void)hipEventDestroy(c->slots[s].done);
       if (c->streams[s]) (void)hipStreamDestroy(c->streams[s]);
     }
     c->ff.release();
@@ -654,6 +743,22 @@ int amph_mask_words(amph_ctx* c, const uint8_t* secrets, const uint8_t* masks, s
                          const amph::LaunchCfg& lc) {
                        return amph::launch_mask_words(din[0], din[1], cnt, dout[0], c->f, lc);
                      });
+}
+
+int amph_host_register(amph_ctx* c, void* ptr, size_t bytes) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (!ptr || !bytes) return fail(AMPH_E_PARAM, "null or empty range");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  return AMPH_OK;
+}
+
+int amph_host_unregister(amph_ctx* c, void* ptr) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (!ptr) return fail(AMPH_E_PARAM, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipHostUnregister(ptr));
+  return AMPH_OK;
 }
 
 int amph_synth_odos(amph_ctx* c, uint64_t seed, int n, size_t words, uint8_t* const* out_fields,

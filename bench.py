@@ -49,7 +49,55 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--mode", choices=["device", "host"], default="device",
+                    help="host: inputs/outputs in host memory (PCIe-inclusive rate, C5)")
+    ap.add_argument("--pin", action="store_true", help="host mode: page-lock the inputs first")
+    ap.add_argument("--batch-words", type=int, default=4 << 20)
     return ap.parse_args()
+
+
+def host_mode(a, A, torch, ctx):
+    """End-to-end host-memory rate (SURVEY.md C5 per GPU): ODOs and secrets
+    live in (pageable or page-locked) host memory; each step streams them
+    through the GPU in --batch-words batches (3-slot HtoD/compute/DtoH
+    pipeline) and writes the masked words and canonical secrets back to host
+    memory.  Not the headline metric; recorded in DESIGN.md."""
+    W, n = a.words, a.parties
+    ctx.set_batch_words(a.batch_words)
+    _, mb, _ = ctx.synth_odos(seed=11, n=n, words=W)
+    mask_h = mb.cpu().numpy()
+    del mb
+    _, sb, _ = ctx.synth_odos(seed=12, n=n, words=W)
+    share_h = sb.cpu().numpy()
+    del sb
+    sec_h = ctx.synth_words(seed=13, count=W).cpu().numpy()
+    torch.cuda.empty_cache()
+    mask_odos = [tuple(mask_h[k, j] for k in range(5)) for j in range(n)]
+    share_odos = [tuple(share_h[k, j] for k in range(5)) for j in range(n)]
+    if a.pin:
+        for arr in (mask_h, share_h, sec_h):
+            ctx.host_register(arr)
+    for _ in range(a.warmup):
+        ctx.mask_input(mask_odos, sec_h)
+        ctx.recombine_verify(share_odos)
+    t0 = time.perf_counter()
+    ok = True
+    for _ in range(a.steps):
+        _, f1 = ctx.mask_input(mask_odos, sec_h)
+        _, f2 = ctx.recombine_verify(share_odos)
+        ok &= f1 == -1 and f2 == -1
+    el = time.perf_counter() - t0
+    hbytes = (kbytes("k_mask", n) + kbytes("k_rv", n)) * W
+    line = {"metric": "secret words/s host-memory share+recombine (PCIe-inclusive)",
+            "value": W * a.steps / el, "unit": "words/s", "n_gpus": 1, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": el * 1e3 / a.steps, "higher_is_better": True,
+            "verified": ok, "pinned_inputs": a.pin, "batch_words": a.batch_words,
+            "host_bytes_per_step": hbytes, "host_GBps": hbytes * a.steps / el / 1e9,
+            "config": {"workload": "K_MASK + K_RV from host memory", "words": W, "parties": n}}
+    print(json.dumps(line), flush=True)
+    if a.pin:
+        for arr in (mask_h, share_h, sec_h):
+            ctx.host_unregister(arr)
 
 
 def cpu_baseline(n: int, budget_s: float):
@@ -95,6 +143,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     ctx = A.Context(TEST_PRIME, TEST_R, TEST_RINV, device=local)
+    if a.mode == "host":
+        return host_mode(a, A, torch, ctx)
     W, n = a.words, a.parties
     mask_odos, mbuf, _ = ctx.synth_odos(seed=1000 + rank, n=n, words=W)
     share_odos, sbuf, _ = ctx.synth_odos(seed=2000 + rank, n=n, words=W)

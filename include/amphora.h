@@ -108,8 +108,16 @@ int amph_ctx_create(const uint8_t p_le[16], const uint8_t r_le[16], const uint8_
                     int device, amph_ctx** out);
 void amph_ctx_destroy(amph_ctx* ctx);
 int amph_ctx_device(const amph_ctx* ctx);
-/* Host-path batch size in words (default 4 Mi); 0 keeps the current value. */
+/* Host-path batch size in words (default 4 Mi); 0 keeps the current value.
+ * Host-pointer calls stream their arrays through the GPU batch by batch:
+ * pageable caller memory is staged through page-locked buffers by CPU
+ * threads (AMPH_HOST_THREADS, default min(8, cores/2)) with HtoD, kernel and
+ * DtoH of consecutive batches overlapped on 3 HIP streams. */
 int amph_ctx_set_batch_words(amph_ctx* ctx, size_t words);
+/* Page-lock a caller buffer (hipHostRegister) so host-pointer calls DMA it
+ * directly without the staging copy (e.g. a long-lived direct ByteBuffer). */
+int amph_host_register(amph_ctx* ctx, void* ptr, size_t bytes);
+int amph_host_unregister(amph_ctx* ctx, void* ptr);
 
 const char* amph_strerror(int status);
 /* Detail of the last error on the calling thread (empty string if none). */

@@ -149,6 +149,29 @@ def test_host_batches_report_global_index(ctx, F):
     assert ff == 1777 and np.array_equal(y, oy)
 
 
+def test_host_stream_pinned_and_pageable(ctx, F):
+    """Many batches through the 3-slot pipeline, pageable and page-locked
+    caller buffers mixed (the staging copy is skipped for the latter)."""
+    W = 70_001
+    odos, buf = F.synth_odos(seed=13, n=2, W=W, fault_index=65_000)
+    secrets = F.synth_words(seed=14, count=W, mont=False)
+    ctx.set_batch_words(8192)
+    try:
+        y1, ff1 = ctx.recombine_verify(odos)
+        ctx.host_register(buf)
+        try:
+            y2, ff2 = ctx.recombine_verify(odos)
+            m2, mf = ctx.mask_input(odos, secrets)
+        finally:
+            ctx.host_unregister(buf)
+    finally:
+        ctx.set_batch_words(4 << 20)
+    oy, off = F.recombine_verify(odos)
+    om, omf = F.mask_input(secrets, odos)
+    assert ff1 == ff2 == off == 65_000 and mf == omf == 65_000
+    assert np.array_equal(y1, oy) and np.array_equal(y2, oy) and np.array_equal(m2, om)
+
+
 def test_empty_and_single(ctx):
     z = np.zeros((0, 16), np.uint8)
     y, ff = ctx.recombine_verify([(z,) * 5, (z,) * 5])
