@@ -1,0 +1,78 @@
+"""Multi-process (world_size 2, gloo on CPU) tests of the data-parallel path:
+contiguous word shards, root scatter / gather of word arrays (RCCL over xGMI
+on the GPU node, gloo here), and the min-combine of the verify verdict.
+The per-shard arithmetic here is the C oracle (CPU); on the GPU node it is
+the HIP kernels (bench.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from amphora_amd.shard import (NO_FAILURE, combine_first_fail, gather_words, global_first_fail,
+                               scatter_words, shard_range)
+
+
+def test_shard_range_covers_exactly():
+    for W in (0, 1, 7, 8, 1000, 1 << 20, 10007):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(W, r, world) for r in range(world)]
+            assert sum(c for _, c in spans) == W
+            pos = 0
+            for s, c in spans:
+                if c:
+                    assert s == pos
+                pos += c
+
+
+def test_global_first_fail():
+    assert global_first_fail(-1, 100) == NO_FAILURE
+    assert global_first_fail(NO_FAILURE, 100) == NO_FAILURE
+    assert global_first_fail(5, 100) == 105
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, W, fault, result_dir):
+    import torch
+    import torch.distributed as dist
+    from oracle import coracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    F = coracle.test_field(threads=1)
+    n = 2
+    like = torch.empty((0, 16), dtype=torch.uint8)
+    fields = []
+    if rank == 0:
+        odos, buf = F.synth_odos(seed=77, n=n, W=W, fault_index=fault)
+        full = [torch.from_numpy(np.ascontiguousarray(buf[k, j])) for k in range(5) for j in range(n)]
+    for idx in range(5 * n):
+        fields.append(scatter_words(full[idx] if rank == 0 else None, W, 16, like=like))
+    start, count = shard_range(W, rank, world)
+    local = [tuple(fields[k * n + j].numpy() for k in range(5)) for j in range(n)]
+    y, ff = F.recombine_verify(local) if count else (np.zeros((0, 16), np.uint8), -1)
+    g = combine_first_fail(ff, start)
+    yfull = gather_words(torch.from_numpy(y), W, 16)
+    if rank == 0:
+        ref_y, ref_ff = F.recombine_verify(odos)
+        ok = g == ref_ff and np.array_equal(yfull.numpy(), ref_y)
+        with open(os.path.join(result_dir, "ok"), "w") as f:
+            f.write("%d %d %d" % (int(ok), g, ref_ff))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W,fault", [(10007, 7777), (10007, 3), (5, -1)])
+def test_scatter_verify_gather_two_ranks(tmp_path, W, fault):
+    import torch.multiprocessing as mp
+    mp.start_processes(_worker, args=(2, _free_port(), W, fault, str(tmp_path)), nprocs=2,
+                       join=True, start_method="spawn")
+    ok, g, ref = open(tmp_path / "ok").read().split()
+    assert ok == "1", (g, ref)
+    assert int(g) == fault

@@ -1,0 +1,52 @@
+"""Per-launch HBM traffic from rocprofv3 PMC passes -> profiles/traffic.json.
+
+    python tools/pmc_traffic.py FETCH_CSV WRITE_CSV --words W --parties N [--out profiles/traffic.json]
+
+FETCH_SIZE and WRITE_SIZE come from separate passes (they cannot share one on
+gfx950).  Per MI355X_MICROARCH.md §HBM, gfx950's FETCH_SIZE reports exactly
+half the bytes of a wide coalesced streaming read, so it is doubled;
+WRITE_SIZE is exact for 16-B-per-lane stores.  Units: KiB.
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+
+
+def per_kernel(path, counter):
+    vals = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            vals[r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_csv")
+    ap.add_argument("write_csv")
+    ap.add_argument("--words", type=int, required=True)
+    ap.add_argument("--parties", type=int, required=True)
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "traffic.json"))
+    a = ap.parse_args()
+    f = per_kernel(a.fetch_csv, "FETCH_SIZE")
+    w = per_kernel(a.write_csv, "WRITE_SIZE")
+    algo = {"k_rv": 80 * a.parties + 16, "k_mask": 80 * a.parties + 32}
+    out = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    for k in ("k_mask", "k_rv"):
+        if k not in f or k not in w:
+            continue
+        fetch = 2 * f[k] * 1024
+        write = w[k] * 1024
+        out["%s_n%d_w%d" % (k, a.parties, a.words)] = {
+            "hbm_bytes_per_launch": fetch + write, "fetch_bytes_corrected": fetch,
+            "write_bytes": write, "algorithmic_bytes": algo[k] * a.words,
+            "ratio_to_algorithmic": (fetch + write) / (algo[k] * a.words),
+            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), FETCH x2 (gfx950)"}
+    json.dump(out, open(a.out, "w"), indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
