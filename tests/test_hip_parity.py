@@ -132,10 +132,17 @@ def test_mask_input_fewer_secrets_than_masks(ctx, F):
     secrets = F.synth_words(seed=8, count=3000, mont=False)
     out, ff = ctx.mask_input(odos, secrets)
     assert ff == 4500  # the verify covers every mask word
+    import torch
+    dodos = [tuple(torch.from_numpy(f).cuda() for f in o) for o in odos]
+    _, dff = ctx.mask_input(dodos, torch.from_numpy(secrets).cuda())
+    assert ff_dev(dff) == 4500  # device path: verify-only tail reports global indices
     odos, _ = F.synth_odos(seed=11, n=2, W=5000)
     out, ff = ctx.mask_input(odos, secrets)
     oo, _ = F.mask_input(secrets, [tuple(f[:3000] for f in o) for o in odos])
     assert ff == -1 and np.array_equal(out, oo)
+    dodos = [tuple(torch.from_numpy(f).cuda() for f in o) for o in odos]
+    dout, dff = ctx.mask_input(dodos, torch.from_numpy(secrets).cuda())
+    assert ff_dev(dff) == -1 and np.array_equal(host(dout), oo)
 
 
 def test_host_batches_report_global_index(ctx, F):
