@@ -1,0 +1,81 @@
+"""BASELINE config C1 end to end: DefaultAmphoraClient.createSecret /
+getSecret against N in-process amphora-service parties (amphora_amd.loopback)
+with a fake Castor dealer -- every word of arithmetic (mask ODOs with Beaver
+multiplications, client verify + masking, share conversion with MACs, share
+ODOs, client recombine + verify) on the HIP kernels."""
+import random
+import uuid
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from oracle import amphora_oracle as O  # noqa: E402
+from tests.loopback_dealer import FakeCastor  # noqa: E402
+
+P, R, RINV = O.TEST_PRIME, O.TEST_R, O.TEST_RINV
+SPDZ = O.MpSpdzIntegrationUtils(P, R, RINV)
+
+
+def _cluster(n, seed):
+    import torch
+    assert torch.cuda.is_available()
+    from amphora_amd.loopback import AmphoraParty, ExchangeHub, LoopbackAmphoraClient
+    rng = random.Random(seed)
+    keys = [rng.randrange(P) for _ in range(n)]
+    castor = FakeCastor(P, R, RINV, keys, seed)
+    hub = ExchangeHub(n)
+    parties = [AmphoraParty(j, P, R, RINV, keys[j], castor, hub) for j in range(n)]
+    return LoopbackAmphoraClient(parties, P, R, RINV), parties, keys, castor
+
+
+@pytest.mark.parametrize("n,W", [(2, 1000), (3, 257), (2, 1)])
+def test_upload_download_roundtrip(n, W):
+    import amphora_amd as A
+    client, parties, keys, castor = _cluster(n, seed=W + n)
+    rng = random.Random(5)
+    data = [rng.randrange(2 ** 63) if i % 2 else rng.randrange(P) for i in range(W)]
+    sid = client.create_secret(A.Secret.of([("k", "v")], data))
+    got = client.get_secret(sid)
+    assert got.data == data
+    # stored shares carry valid SPDZ MACs: sum(mac) == alpha * sum(value)
+    alpha = sum(keys) % P
+    for i in range(W):
+        val = sum(SPDZ.from_gfp(p.secrets[sid].data[32 * i:32 * i + 16]) for p in parties) % P
+        mac = sum(SPDZ.from_gfp(p.secrets[sid].data[32 * i + 16:32 * i + 32]) for p in parties) % P
+        assert val == data[i] % P and mac == alpha * val % P
+    # tuple requests follow the reference's ids (InputMaskCachingService :92-93,
+    # OutputDeliveryService :140-141)
+    odo_req = O.odo_request_id(sid)
+    assert any(c[1] == odo_req for c in castor.calls)
+    assert any(c[1] == O.operation_id(odo_req, 2 * W) for c in castor.calls)
+    client.close()
+
+
+def test_tampered_party_is_detected():
+    import amphora_amd as A
+    client, parties, _, _ = _cluster(2, seed=9)
+    data = list(range(1, 101))
+    sid = client.create_secret(A.Secret.of([], data))
+    victim = parties[1]
+    orig = victim.get_secret_share
+
+    def tampered(secret_id, request_id):
+        odo = orig(secret_id, request_id)
+        y = bytearray(odo.secret_shares)
+        y[16 * 42] ^= 0x01  # a malicious party shifts one secret share
+        return A.OutputDeliveryObject(bytes(y), odo.r_shares, odo.v_shares, odo.w_shares, odo.u_shares)
+
+    victim.get_secret_share = tampered
+    with pytest.raises(A.IntegrityVerificationException, match="^Verification of secret has failed"):
+        client.get_secret(sid)
+    client.close()
+
+
+def test_upload_without_masks_fails():
+    import amphora_amd as A
+    client, parties, _, _ = _cluster(2, seed=3)
+    mi = A.MaskedInput(uuid.uuid4(), [A.MaskedInputData.of(bytes(16))], [])
+    with pytest.raises(A.AmphoraServiceException, match="No input masks found"):
+        parties[0].upload_masked_input(mi)
+    client.close()
