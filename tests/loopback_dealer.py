@@ -7,6 +7,7 @@ three shares) with Python ints, one stream per party, cached per
 -- what Castor guarantees across VCPs.
 """
 import random
+import threading
 
 from oracle.amphora_oracle import MpSpdzIntegrationUtils
 
@@ -24,6 +25,7 @@ class FakeCastor:
         self.rng = random.Random(seed)
         self.cache = {}
         self.calls = []
+        self._lock = threading.Lock()  # parties call concurrently
 
     def _share(self, x):
         sh = [self.rng.randrange(self.p) for _ in range(self.n - 1)]
@@ -35,6 +37,10 @@ class FakeCastor:
         return list(zip(self._share(x), self._share(self.alpha * x % self.p)))
 
     def __call__(self, player, request_id, ttype, count):
+        with self._lock:
+            return self._get(player, request_id, ttype, count)
+
+    def _get(self, player, request_id, ttype, count):
         self.calls.append((player, request_id, ttype, count))
         key = (request_id, ttype)
         if key not in self.cache:
