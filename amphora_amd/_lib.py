@@ -72,6 +72,7 @@ def _load():
     L.amph_odo_post.argtypes = [vp, vp, vp, sz, i32, vp, vp, u32, vp]
     L.amph_host_register.argtypes = [vp, vp, sz]
     L.amph_host_unregister.argtypes = [vp, vp]
+    L.amph_time_next_launch.argtypes = [vp, vp]
     L.amph_synth_odos.argtypes = [vp, u64, i32, sz, C.POINTER(vp), vp, C.c_int64, i32, vp]
     L.amph_synth_words.argtypes = [vp, u64, sz, vp, vp]
     return L
@@ -84,7 +85,8 @@ EXPORTED = ["amph_ctx_create", "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_
             "amph_mask_input", "amph_recombine", "amph_verify", "amph_verify_message",
             "amph_mask_words", "amph_to_gfp", "amph_from_gfp", "amph_convert_share",
             "amph_odo_pre", "amph_open_diffs", "amph_odo_post", "amph_synth_odos",
-            "amph_synth_words", "amph_host_register", "amph_host_unregister"]
+            "amph_synth_words", "amph_host_register", "amph_host_unregister",
+            "amph_time_next_launch"]
 
 
 class _AmphOdo(C.Structure):

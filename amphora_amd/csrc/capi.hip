@@ -29,6 +29,7 @@ using amph::W4;
 namespace {
 
 thread_local std::string g_last_error;
+thread_local hipEvent_t g_ev_start = nullptr, g_ev_stop = nullptr;  // amph_time_next_launch
 
 int fail(int status, const std::string& msg) {
   g_last_error = msg;
@@ -168,7 +169,11 @@ int block_for(const amph_ctx* c, size_t words) {
 }
 
 amph::LaunchCfg cfg(amph_ctx* c, hipStream_t s, size_t words) {
-  return amph::LaunchCfg{s, c->grid_cap, block_for(c, words)};
+  amph::LaunchCfg lc{s, c->grid_cap, block_for(c, words)};
+  lc.ev_start = g_ev_start;  // consumed by this launch only
+  lc.ev_stop = g_ev_stop;
+  g_ev_start = g_ev_stop = nullptr;
+  return lc;
 }
 
 // ---- host batching ------------------------------------------------------------
@@ -359,6 +364,12 @@ int reset_ff_dev(int64_t* ff, uint32_t flags, hipStream_t s) {
 
 // ============================================================================
 extern "C" {
+
+int amph_time_next_launch(void* start_event, void* stop_event) {
+  g_ev_start = (hipEvent_t)start_event;
+  g_ev_stop = (hipEvent_t)stop_event;
+  return AMPH_OK;
+}
 
 const char* amph_version(void) { return "amphora_amd 0.1.0 (gfx950)"; }
 

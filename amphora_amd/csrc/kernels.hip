@@ -16,7 +16,15 @@
 //   k_odo_post   A9 post + A8     OutputDeliveryService.java:147-152,274-286
 #include "kernels.hpp"
 
+#include <hip/hip_ext.h>
+
 namespace amph {
+
+// Every launch goes through hipExtLaunchKernelGGL: with the config's timing
+// events set (amph_time_next_launch) the events are stamped by the kernel's
+// own dispatch, i.e. they measure the kernel, not the queue gap before it.
+#define AMPH_LAUNCH(K, G, B, C, ...) \
+  hipExtLaunchKernelGGL(K, G, B, 0, (C).stream, (C).ev_start, (C).ev_stop, 0, __VA_ARGS__)
 
 namespace {
 
@@ -352,7 +360,7 @@ hipError_t launch_recombine_verify(const OdoSet& odo, int n, size_t words, uint4
                                    unsigned long long* ff, const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-#define L(NP, BIG) hipLaunchKernelGGL((k_rv<NP, BIG>), dim3(g), dim3(c.block), 0, c.stream, odo, n, words, out_y, ff, f, (size_t)0)
+#define L(NP, BIG) AMPH_LAUNCH((k_rv<NP, BIG>), dim3(g), dim3(c.block), c, odo, n, words, out_y, ff, f, (size_t)0)
   if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
   return hipGetLastError();
@@ -364,7 +372,9 @@ hipError_t launch_mask_input(const OdoSet& odo, int n, size_t words, const uint4
   if (n_secrets > words) n_secrets = words;
   if (n_secrets > 0) {
     const unsigned g = grid_for(n_secrets, c);
-#define L(NP, BIG) hipLaunchKernelGGL((k_mask<NP, BIG>), dim3(g), dim3(c.block), 0, c.stream, odo, n, n_secrets, secrets, out, ff, f)
+    LaunchCfg c1 = c;  // timing events bracket both launches when there is a tail
+    if (words > n_secrets) c1.ev_stop = nullptr;
+#define L(NP, BIG) AMPH_LAUNCH((k_mask<NP, BIG>), dim3(g), dim3(c.block), c1, odo, n, n_secrets, secrets, out, ff, f)
     if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
     hipError_t e = hipGetLastError();
@@ -377,7 +387,9 @@ hipError_t launch_mask_input(const OdoSet& odo, int n, size_t words, const uint4
       for (int j = 0; j < n; ++j) tail.f[k][j] = odo.f[k][j] + n_secrets;
     const size_t tw = words - n_secrets;
     const unsigned g = grid_for(tw, c);
-#define L(NP, BIG) hipLaunchKernelGGL((k_rv<NP, BIG, false>), dim3(g), dim3(c.block), 0, c.stream, tail, n, tw, (uint4*)nullptr, ff, f, n_secrets)
+    LaunchCfg c2 = c;
+    if (n_secrets > 0) c2.ev_start = nullptr;
+#define L(NP, BIG) AMPH_LAUNCH((k_rv<NP, BIG, false>), dim3(g), dim3(c.block), c2, tail, n, tw, (uint4*)nullptr, ff, f, n_secrets)
     if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
   }
@@ -388,7 +400,7 @@ hipError_t launch_recombine(const ShareSet& sh, int n, size_t words, uint4* out,
                             const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-#define L(NP, BIG) hipLaunchKernelGGL((k_recombine<NP, BIG>), dim3(g), dim3(c.block), 0, c.stream, sh, n, words, out, f)
+#define L(NP, BIG) AMPH_LAUNCH((k_recombine<NP, BIG>), dim3(g), dim3(c.block), c, sh, n, words, out, f)
   if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
   return hipGetLastError();
@@ -399,8 +411,8 @@ hipError_t launch_verify(const uint4* y, const uint4* r, const uint4* u, const u
                          const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-  if (f.big) hipLaunchKernelGGL((k_verify<true>), dim3(g), dim3(c.block), 0, c.stream, y, r, u, v, w, words, ff, f);
-  else hipLaunchKernelGGL((k_verify<false>), dim3(g), dim3(c.block), 0, c.stream, y, r, u, v, w, words, ff, f);
+  if (f.big) AMPH_LAUNCH((k_verify<true>), dim3(g), dim3(c.block), c, y, r, u, v, w, words, ff, f);
+  else AMPH_LAUNCH((k_verify<false>), dim3(g), dim3(c.block), c, y, r, u, v, w, words, ff, f);
   return hipGetLastError();
 }
 
@@ -408,8 +420,8 @@ hipError_t launch_convert_share(const uint4* masked, const uint4* tuples, size_t
                                 int use_zero, uint4* out, const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-  if (f.big) hipLaunchKernelGGL((k_conv<true>), dim3(g), dim3(c.block), 0, c.stream, masked, tuples, words, alpha, use_zero, out, f);
-  else hipLaunchKernelGGL((k_conv<false>), dim3(g), dim3(c.block), 0, c.stream, masked, tuples, words, alpha, use_zero, out, f);
+  if (f.big) AMPH_LAUNCH((k_conv<true>), dim3(g), dim3(c.block), c, masked, tuples, words, alpha, use_zero, out, f);
+  else AMPH_LAUNCH((k_conv<false>), dim3(g), dim3(c.block), c, masked, tuples, words, alpha, use_zero, out, f);
   return hipGetLastError();
 }
 
@@ -417,7 +429,7 @@ hipError_t launch_odo_pre(const uint4* share_data, int stride_w, const uint4* ma
                           const uint4* triples, size_t words, uint4* oy, uint4* orr, uint4* ov,
                           uint4* omag, uint32_t* oneg, const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_odo_pre, dim3(grid_for(words, c)), dim3(c.block), 0, c.stream, share_data,
+  AMPH_LAUNCH(k_odo_pre, dim3(grid_for(words, c)), dim3(c.block), c, share_data,
                      stride_w, masks, triples, words, oy, orr, ov, omag, oneg, f);
   return hipGetLastError();
 }
@@ -426,7 +438,7 @@ hipError_t launch_open_diffs(const SignedSet& d, int n, size_t words, uint4* out
                              const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-#define L(NP, BIG) hipLaunchKernelGGL((k_open<NP, BIG>), dim3(g), dim3(c.block), 0, c.stream, d, n, words, out, f)
+#define L(NP, BIG) AMPH_LAUNCH((k_open<NP, BIG>), dim3(g), dim3(c.block), c, d, n, words, out, f)
   if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
   return hipGetLastError();
@@ -436,8 +448,8 @@ hipError_t launch_odo_post(const uint4* opened, const uint4* triples, size_t wor
                            uint4* ow, uint4* ou, const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-  if (f.big) hipLaunchKernelGGL((k_odo_post<true>), dim3(g), dim3(c.block), 0, c.stream, opened, triples, words, p0, ow, ou, f);
-  else hipLaunchKernelGGL((k_odo_post<false>), dim3(g), dim3(c.block), 0, c.stream, opened, triples, words, p0, ow, ou, f);
+  if (f.big) AMPH_LAUNCH((k_odo_post<true>), dim3(g), dim3(c.block), c, opened, triples, words, p0, ow, ou, f);
+  else AMPH_LAUNCH((k_odo_post<false>), dim3(g), dim3(c.block), c, opened, triples, words, p0, ow, ou, f);
   return hipGetLastError();
 }
 
@@ -445,15 +457,15 @@ hipError_t launch_to_gfp(const uint4* in, size_t words, uint4* out, const Fp& f,
                          const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-  if (f.big) hipLaunchKernelGGL((k_to_gfp<true>), dim3(g), dim3(c.block), 0, c.stream, in, words, out, f);
-  else hipLaunchKernelGGL((k_to_gfp<false>), dim3(g), dim3(c.block), 0, c.stream, in, words, out, f);
+  if (f.big) AMPH_LAUNCH((k_to_gfp<true>), dim3(g), dim3(c.block), c, in, words, out, f);
+  else AMPH_LAUNCH((k_to_gfp<false>), dim3(g), dim3(c.block), c, in, words, out, f);
   return hipGetLastError();
 }
 
 hipError_t launch_from_gfp(const uint4* in, size_t words, uint4* out, const Fp& f,
                            const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_from_gfp, dim3(grid_for(words, c)), dim3(c.block), 0, c.stream, in, words, out, f);
+  AMPH_LAUNCH(k_from_gfp, dim3(grid_for(words, c)), dim3(c.block), c, in, words, out, f);
   return hipGetLastError();
 }
 
@@ -461,8 +473,8 @@ hipError_t launch_mask_words(const uint4* secrets, const uint4* masks, size_t wo
                              const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-  if (f.big) hipLaunchKernelGGL((k_mask_words<true>), dim3(g), dim3(c.block), 0, c.stream, secrets, masks, words, out, f);
-  else hipLaunchKernelGGL((k_mask_words<false>), dim3(g), dim3(c.block), 0, c.stream, secrets, masks, words, out, f);
+  if (f.big) AMPH_LAUNCH((k_mask_words<true>), dim3(g), dim3(c.block), c, secrets, masks, words, out, f);
+  else AMPH_LAUNCH((k_mask_words<false>), dim3(g), dim3(c.block), c, secrets, masks, words, out, f);
   return hipGetLastError();
 }
 
@@ -471,8 +483,8 @@ hipError_t launch_synth_odos(const OutSet& out, int n, size_t words, uint64_t se
                              const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
   const unsigned g = grid_for(words, c);
-  if (f.big) hipLaunchKernelGGL((k_synth<true>), dim3(g), dim3(c.block), 0, c.stream, out, n, words, seed, plain_y, fault, permille, f);
-  else hipLaunchKernelGGL((k_synth<false>), dim3(g), dim3(c.block), 0, c.stream, out, n, words, seed, plain_y, fault, permille, f);
+  if (f.big) AMPH_LAUNCH((k_synth<true>), dim3(g), dim3(c.block), c, out, n, words, seed, plain_y, fault, permille, f);
+  else AMPH_LAUNCH((k_synth<false>), dim3(g), dim3(c.block), c, out, n, words, seed, plain_y, fault, permille, f);
   return hipGetLastError();
 }
 
@@ -480,8 +492,8 @@ hipError_t launch_synth_words(uint4* out, size_t count, uint64_t seed, const Fp&
                               const LaunchCfg& c) {
   if (count == 0) return hipSuccess;
   const unsigned g = grid_for(count, c);
-  if (f.big) hipLaunchKernelGGL((k_synth_words<true>), dim3(g), dim3(c.block), 0, c.stream, out, count, seed, f);
-  else hipLaunchKernelGGL((k_synth_words<false>), dim3(g), dim3(c.block), 0, c.stream, out, count, seed, f);
+  if (f.big) AMPH_LAUNCH((k_synth_words<true>), dim3(g), dim3(c.block), c, out, count, seed, f);
+  else AMPH_LAUNCH((k_synth_words<false>), dim3(g), dim3(c.block), c, out, count, seed, f);
   return hipGetLastError();
 }
 

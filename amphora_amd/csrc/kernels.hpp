@@ -32,6 +32,8 @@ struct LaunchCfg {
   hipStream_t stream;
   int grid_cap;  // 0 = full grid (one word per thread); > 0 caps it (grid-stride beyond)
   int block;     // threads per workgroup, multiple of 64, <= kMaxBlock
+  hipEvent_t ev_start = nullptr;  // optional: stamped by the kernel dispatch itself
+  hipEvent_t ev_stop = nullptr;
 };
 
 // K_RV: recombine 5 fields over n parties, verify w == y r, u == v r,

@@ -272,14 +272,14 @@ def main():
     step_no = [0]
 
     def step(ev=None):
+        # kernel timing: hipExtLaunchKernel stamps the events at each kernel's
+        # own dispatch start/end (amph_time_next_launch), on the launch stream
         if ev is not None:
-            ev[0].record()
+            lib.lib.amph_time_next_launch(ev[0].cuda_event, ev[1].cuda_event)
         k_mask()
         if ev is not None:
-            ev[1].record()
+            lib.lib.amph_time_next_launch(ev[2].cuda_event, ev[3].cuda_event)
         k_rv()
-        if ev is not None:
-            ev[2].record()
         if distributed:
             v = verdicts[step_no[0]:step_no[0] + 1]
             v.copy_(ff.min().view(1))
@@ -292,7 +292,11 @@ def main():
         w.wait()
     works.clear()
     torch.cuda.synchronize()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(a.steps)]
+    for evs in events:  # create the underlying hipEvents (torch creates lazily)
+        for e in evs:
+            e.record()
+    torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -306,7 +310,7 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     t_mask = sum(e[0].elapsed_time(e[1]) for e in events) / a.steps  # ms per launch
-    t_rv = sum(e[1].elapsed_time(e[2]) for e in events) / a.steps
+    t_rv = sum(e[2].elapsed_time(e[3]) for e in events) / a.steps
     fails = [int(x) for x in ff.cpu().tolist()]
     if distributed:
         t = torch.tensor([el, t_mask, t_rv], dtype=torch.float64, device="cuda")

@@ -119,6 +119,12 @@ int amph_ctx_set_batch_words(amph_ctx* ctx, size_t words);
 int amph_host_register(amph_ctx* ctx, void* ptr, size_t bytes);
 int amph_host_unregister(amph_ctx* ctx, void* ptr);
 
+/* Kernel timing: the next kernel launch made by an amph_* call on the
+ * calling thread records these hipEvent_t's (created, timing-enabled) at its
+ * own dispatch start / end (hipExtLaunchKernel), so hipEventElapsedTime
+ * measures the kernel alone.  Either may be NULL.  Used by bench.py. */
+int amph_time_next_launch(void* start_event, void* stop_event);
+
 const char* amph_strerror(int status);
 /* Detail of the last error on the calling thread (empty string if none). */
 const char* amph_last_error(void);
