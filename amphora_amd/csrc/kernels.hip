@@ -168,75 +168,121 @@ __device__ __forceinline__ uint32_t signed_diff(const W4& x, const W4& a, W4& ma
   return neg;
 }
 
-__global__ __launch_bounds__(kMaxBlock) void k_odo_pre(const uint4* share_data, int stride_w,
-                                                   const uint4* masks, const uint4* triples,
-                                                   size_t words, uint4* oy, uint4* orr, uint4* ov,
-                                                   uint4* omag, uint32_t* oneg, Fp f) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
-    const uint4 yr = ld(share_data + (size_t)stride_w * i);
-    const uint4 m1 = ld(masks + 4 * i), m2 = ld(masks + 4 * i + 2);
-    const uint4* t0 = triples + 12 * i;  // triple 2i: a = t0[0], b = t0[2]
-    const uint4 a0 = ld(t0), b0 = ld(t0 + 2), a1 = ld(t0 + 6), b1 = ld(t0 + 8);
+// AoS tuple staging: a workgroup's contiguous run of tuples (S uint4 each) is
+// read with fully coalesced 16-B loads (consecutive lanes, consecutive uint4)
+// into LDS at a padded stride of S+1 uint4 (breaks the power-of-two bank
+// pattern of the per-lane reads), then each lane reads its own tuple's fields.
+template <int S, int BS>
+__device__ __forceinline__ void stage_tuples(uint4* lds, const uint4* src, size_t ntuples) {
+#pragma unroll
+  for (int r = 0; r < S; ++r) {
+    const size_t q = (size_t)r * BS + threadIdx.x;
+    if (q < (size_t)S * ntuples) lds[(q / S) * (S + 1) + q % S] = ld(src + q);
+  }
+}
+
+constexpr int kPairBlock = 256;  // pairs per workgroup of the LDS-staged kernels
+
+// K_ODO_PRE, one Beaver pair per lane (k = 2i: (y_i, r_i), k = 2i+1: (v_i, r_i);
+// r_i = value of mask tuple 2i, v_i = value of mask tuple 2i+1), the
+// workgroup's triples (96 B) and mask tuples (32 B) staged through LDS.
+// Even lanes also write the raw y_i and r_i copies, odd lanes v_i.
+__global__ __launch_bounds__(kPairBlock) void k_odo_pre(const uint4* share_data, int stride_w,
+                                                       const uint4* masks, const uint4* triples,
+                                                       size_t pairs, uint4* oy, uint4* orr,
+                                                       uint4* ov, uint4* omag, uint16_t* oneg,
+                                                       Fp f) {
+  __shared__ uint4 tri[kPairBlock * 7];
+  __shared__ uint4 msk[kPairBlock * 3];
+  const size_t k0 = (size_t)blockIdx.x * kPairBlock;
+  const size_t k = k0 + threadIdx.x;
+  const size_t nblk = min((size_t)kPairBlock, pairs - k0);
+  stage_tuples<6, kPairBlock>(tri, triples + 6 * k0, nblk);
+  stage_tuples<2, kPairBlock>(msk, masks + 2 * k0, nblk);
+  const size_t i = k >> 1;
+  const bool even = (k & 1) == 0;
+  uint4 yr = make_uint4(0, 0, 0, 0);
+  if (k < pairs && even) yr = ld(share_data + (size_t)stride_w * i);
+  __syncthreads();
+  if (k >= pairs) return;
+  const unsigned lk = threadIdx.x, lpair0 = lk & ~1u;
+  const uint4 a = tri[lk * 7], b = tri[lk * 7 + 2];
+  const uint4 m1 = msk[lpair0 * 3], m2 = msk[(lpair0 + 1) * 3];
+  const uint4 x = even ? yr : m2;
+  if (even) {
     oy[i] = yr;
     orr[i] = m1;
+  } else {
     ov[i] = m2;
-    const W4 Y = redc(w4(yr), f), M1 = redc(w4(m1), f), M2 = redc(w4(m2), f);
-    W4 d0, e0, d1, e1;
-    const uint32_t s0 = signed_diff(Y, redc(w4(a0), f), d0);
-    const uint32_t s1 = signed_diff(M1, redc(w4(b0), f), e0);
-    const uint32_t s2 = signed_diff(M2, redc(w4(a1), f), d1);
-    const uint32_t s3 = signed_diff(M1, redc(w4(b1), f), e1);
-    st(omag + 4 * i + 0, d0);
-    st(omag + 4 * i + 1, e0);
-    st(omag + 4 * i + 2, d1);
-    st(omag + 4 * i + 3, e1);
-    oneg[i] = s0 | (s1 << 8) | (s2 << 16) | (s3 << 24);
   }
+  W4 d, e;
+  const uint32_t sd = signed_diff(redc(w4(x), f), redc(w4(a), f), d);
+  const uint32_t se = signed_diff(redc(w4(m1), f), redc(w4(b), f), e);
+  st(omag + 2 * k, d);
+  st(omag + 2 * k + 1, e);
+  oneg[k] = (uint16_t)(sd | (se << 8));
 }
 
+// recombineDiffs: one opened value per lane (value t of 4 per source word),
+// so every load and store is a consecutive 16-B (or 1-B sign) access
+// (3x the bandwidth of a word-per-lane mapping, tools/ubench/ubench_party.hip).
 template <int NP, bool BIG>
-__global__ __launch_bounds__(kMaxBlock) void k_open(SignedSet d, int n, size_t words, uint4* out,
+__global__ __launch_bounds__(kMaxBlock) void k_open(SignedSet d, int n, size_t nvals, uint4* out,
                                                 Fp f) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
-  const int np = NP > 0 ? NP : n;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
-    W4 acc[4] = {};
-    for (int j = 0; j < np; ++j) {
-      const uint32_t s = d.neg[j][i];
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < nvals; t += stride) {
+    W4 acc = {};
+    if constexpr (NP > 0) {
+      uint4 m[NP];
+      uint8_t s[NP];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const W4 m = canon<BIG>(w4(ld(d.mag[j] + 4 * i + c)), f);
-        acc[c] = ((s >> (8 * c)) & 0xFF) ? mod_sub(acc[c], m, f) : mod_add(acc[c], m, f);
+      for (int j = 0; j < NP; ++j) {
+        m[j] = ld(d.mag[j] + t);
+        s[j] = reinterpret_cast<const uint8_t*>(d.neg[j])[t];
+      }
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        const W4 x = canon<BIG>(w4(m[j]), f);
+        acc = s[j] ? mod_sub(acc, x, f) : mod_add(acc, x, f);
+      }
+    } else {
+      for (int j = 0; j < n; ++j) {
+        const W4 x = canon<BIG>(w4(ld(d.mag[j] + t)), f);
+        acc = reinterpret_cast<const uint8_t*>(d.neg[j])[t] ? mod_sub(acc, x, f) : mod_add(acc, x, f);
       }
     }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) st(out + 4 * i + c, acc[c]);
+    st(out + t, acc);
   }
 }
 
+// K_ODO_POST, one Beaver pair per lane: z_k = c + [D] b + [E] a (+ [D][E] for
+// player 0) in the Montgomery domain ([D] = mont_mul(D, R^2)); the
+// workgroup's triples staged through LDS (2x the direct strided loads at
+// 16 Mi words, tools/ubench/ubench_party.hip).  Even k -> w, odd k -> u.
 template <bool BIG>
-__global__ __launch_bounds__(kMaxBlock) void k_odo_post(const uint4* opened, const uint4* triples,
-                                                    size_t words, int p0, uint4* ow, uint4* ou,
-                                                    Fp f) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  const W4 r2 = r2_word(f);
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
-    W4 z[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint4* t = triples + 12 * i + 6 * h;
-      const W4 a = w4(ld(t)), b = w4(ld(t + 2)), c = w4(ld(t + 4));
-      const W4 D = mont_mul(w4(ld(opened + 4 * i + 2 * h)), r2, f);
-      const W4 E = mont_mul(w4(ld(opened + 4 * i + 2 * h + 1)), r2, f);
-      W4 acc = mod_add(canon<BIG>(c, f), mont_mul(D, b, f), f);
-      acc = mod_add(acc, mont_mul(E, a, f), f);
-      if (p0) acc = mod_add(acc, mont_mul(D, E, f), f);
-      z[h] = acc;
-    }
-    st(ow + i, z[0]);
-    st(ou + i, z[1]);
+__global__ __launch_bounds__(kPairBlock) void k_odo_post(const uint4* opened,
+                                                        const uint4* triples, size_t pairs,
+                                                        int p0, uint4* ow, uint4* ou, Fp f) {
+  __shared__ uint4 tri[kPairBlock * 7];
+  const size_t k0 = (size_t)blockIdx.x * kPairBlock;
+  const size_t k = k0 + threadIdx.x;
+  const size_t nblk = min((size_t)kPairBlock, pairs - k0);
+  stage_tuples<6, kPairBlock>(tri, triples + 6 * k0, nblk);
+  uint4 Dr = make_uint4(0, 0, 0, 0), Er = Dr;
+  if (k < pairs) {
+    Dr = ld(opened + 2 * k);
+    Er = ld(opened + 2 * k + 1);
   }
+  __syncthreads();
+  if (k >= pairs) return;
+  const W4 a = w4(tri[threadIdx.x * 7]), b = w4(tri[threadIdx.x * 7 + 2]);
+  const W4 c = w4(tri[threadIdx.x * 7 + 4]);
+  const W4 r2 = r2_word(f);
+  const W4 D = mont_mul(w4(Dr), r2, f), E = mont_mul(w4(Er), r2, f);
+  W4 z = mod_add(canon<BIG>(c, f), mont_mul(D, b, f), f);
+  z = mod_add(z, mont_mul(E, a, f), f);
+  if (p0) z = mod_add(z, mont_mul(D, E, f), f);
+  st((k & 1 ? ou : ow) + (k >> 1), z);
 }
 
 // MpSpdzIntegrationUtils.toGfp / fromGfp over arrays, and maskInput with
@@ -429,16 +475,18 @@ hipError_t launch_odo_pre(const uint4* share_data, int stride_w, const uint4* ma
                           const uint4* triples, size_t words, uint4* oy, uint4* orr, uint4* ov,
                           uint4* omag, uint32_t* oneg, const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
-  AMPH_LAUNCH(k_odo_pre, dim3(grid_for(words, c)), dim3(c.block), c, share_data,
-                     stride_w, masks, triples, words, oy, orr, ov, omag, oneg, f);
+  const size_t pairs = 2 * words;
+  AMPH_LAUNCH(k_odo_pre, dim3((unsigned)((pairs + kPairBlock - 1) / kPairBlock)), dim3(kPairBlock), c,
+              share_data, stride_w, masks, triples, pairs, oy, orr, ov, omag, (uint16_t*)oneg, f);
   return hipGetLastError();
 }
 
 hipError_t launch_open_diffs(const SignedSet& d, int n, size_t words, uint4* out, const Fp& f,
                              const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
-  const unsigned g = grid_for(words, c);
-#define L(NP, BIG) AMPH_LAUNCH((k_open<NP, BIG>), dim3(g), dim3(c.block), c, d, n, words, out, f)
+  const size_t nvals = 4 * words;
+  const unsigned g = grid_for(nvals, c);
+#define L(NP, BIG) AMPH_LAUNCH((k_open<NP, BIG>), dim3(g), dim3(c.block), c, d, n, nvals, out, f)
   if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
   return hipGetLastError();
@@ -447,9 +495,10 @@ hipError_t launch_open_diffs(const SignedSet& d, int n, size_t words, uint4* out
 hipError_t launch_odo_post(const uint4* opened, const uint4* triples, size_t words, int p0,
                            uint4* ow, uint4* ou, const Fp& f, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
-  const unsigned g = grid_for(words, c);
-  if (f.big) AMPH_LAUNCH((k_odo_post<true>), dim3(g), dim3(c.block), c, opened, triples, words, p0, ow, ou, f);
-  else AMPH_LAUNCH((k_odo_post<false>), dim3(g), dim3(c.block), c, opened, triples, words, p0, ow, ou, f);
+  const size_t pairs = 2 * words;
+  const dim3 g((unsigned)((pairs + kPairBlock - 1) / kPairBlock));
+  if (f.big) AMPH_LAUNCH((k_odo_post<true>), g, dim3(kPairBlock), c, opened, triples, pairs, p0, ow, ou, f);
+  else AMPH_LAUNCH((k_odo_post<false>), g, dim3(kPairBlock), c, opened, triples, pairs, p0, ow, ou, f);
   return hipGetLastError();
 }
 
