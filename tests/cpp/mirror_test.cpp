@@ -1,0 +1,158 @@
+// C++ host-mirror test (include/amphora.hpp).  Mode "cpu": host-only checks
+// (context validation, decimal parsing, message format).  Mode "gpu": the
+// reference's KATs and a round trip through the GPU kernels.
+//   KAT-1  amphora-service/.../calculation/SecretShareUtilTest.java:68-107
+//   KAT-3  amphora-java-client/.../SecretShareUtilTest.java:30-85
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <string>
+
+#include "amphora.hpp"
+
+using namespace amphora;
+
+static int failures = 0;
+#define EXPECT(c)                                                     \
+  do {                                                                \
+    if (!(c)) {                                                       \
+      std::fprintf(stderr, "FAILED %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      ++failures;                                                     \
+    }                                                                 \
+  } while (0)
+
+static const u128 P = fromDecimal("198766463529478683931867765928436695041", ~(u128)0);
+static const u128 R = fromDecimal("141515903391459779531506841503331516415", ~(u128)0);
+static const u128 RI = fromDecimal("133854242216446749056083838363708373830", ~(u128)0);
+
+static void cpu_tests() {
+  Context c(P, R, RI);
+  EXPECT(toDecimal(P) == "198766463529478683931867765928436695041");
+  EXPECT(fromDecimal("-1", P) == P - 1);
+  EXPECT(fromDecimal("-33717010807885571165607137982809795379", P) ==
+         P - fromDecimal("33717010807885571165607137982809795379", P));
+  bool threw = false;
+  try {
+    Context bad(P, R + 1, RI);
+  } catch (const NativeError& e) {
+    threw = e.status == AMPH_E_PARAM;
+  }
+  EXPECT(threw);
+  auto util = client::SecretShareUtil::of(P, R, RI);
+  EXPECT(util.message(5, 7, 21, 3, 36) ==
+         "Verification of secret has failed:\n\t36 = 5 * 7   &&   21 = 3 * 7\n\t36 = 35   &&   21 = 21");
+  threw = false;
+  try {
+    OutputDeliveryObject o(Bytes(16), Bytes(16), Bytes(32), Bytes(16), Bytes(16));
+  } catch (const IllegalArgumentException& e) {
+    threw = std::string(e.what()) == "The provided shares must be of the same length";
+  }
+  EXPECT(threw);
+}
+
+static void gpu_tests() {
+  auto util = client::SecretShareUtil::of(P, R, RI);
+  const Context& c = util.context();
+  // KAT-1
+  service::SecretShareUtil ssu(c);
+  auto v = [&](const char* d) { return fromDecimal(d, P); };
+  const u128 key = v("-33717010807885571165607137982809795379");
+  Bytes masked = c.toGfp({v("37371993412255263319479925008425883363"), 0});
+  Bytes masks = c.toGfp({v("-82730997414791468496799367418496881908"), v("-60557275363670854182192939229091375859"),
+                         v("45359004002536205186084333850157344582"), v("-48604663536222227589564560476962533035")});
+  Bytes expected = c.toGfp({v("-45359004002536205177319442410070998545"), v("-170814686092998134911558977038957876158"),
+                            v("45359004002536205186084333850157344582"), v("-48604663536222227589564560476962533035")});
+  std::vector<Bytes> mi = {Bytes(masked.begin(), masked.begin() + 16), Bytes(masked.begin() + 16, masked.end())};
+  EXPECT(ssu.convertToSecretShare(mi, toDecimal(key), masks, false) == expected);
+  bool threw = false;
+  try {
+    ssu.convertToSecretShare({Bytes(16)}, "", Bytes(), false);
+  } catch (const IllegalArgumentException& e) {
+    threw = std::string(e.what()) == "Received more input data than available inputMasks.";
+  }
+  EXPECT(threw);
+  // KAT-3 structure: w = s r, u = v r unreduced (< p) pass; w[last] -= 10 fails
+  std::mt19937_64 rng(42);
+  auto nl = [&]() { return (u128)(rng() >> 1); };
+  std::vector<u128> s, r, vv, w, u;
+  for (int i = 0; i < 5; ++i) {
+    s.push_back(nl()); r.push_back(nl()); vv.push_back(nl());
+    w.push_back(s[i] * r[i]); u.push_back(vv[i] * r[i]);
+  }
+  util.verifySecrets(s, r, u, vv, w);
+  w[4] -= 10;
+  threw = false;
+  try {
+    util.verifySecrets(s, r, u, vv, w);
+  } catch (const IntegrityVerificationException& e) {
+    threw = std::string(e.what()).rfind("Verification of secret has failed", 0) == 0;
+  }
+  EXPECT(threw);
+  // round trip: 2-party ODOs of secrets, recombine + verify recovers them
+  const size_t W = 777;
+  std::vector<u128> sec(W), share0[5], share1[5];
+  for (size_t i = 0; i < W; ++i) sec[i] = ((u128)rng() << 64 | rng()) % P;
+  std::vector<u128> rr(W), vr(W);
+  for (size_t i = 0; i < W; ++i) { rr[i] = ((u128)rng() << 64 | rng()) % P; vr[i] = rng(); }
+  // test data: w = s r mod p by a host double-and-add ladder (independent of
+  // the kernels' Montgomery products)
+  auto mulmod = [&](u128 a, u128 b) {
+    u128 acc = 0;
+    for (int bit = 127; bit >= 0; --bit) {
+      acc = addMod(acc, acc, P);
+      if ((b >> bit) & 1) acc = addMod(acc, a % P, P);
+    }
+    return acc;
+  };
+  std::vector<u128> vals[5];
+  for (size_t i = 0; i < W; ++i) {
+    vals[0].push_back(sec[i]); vals[1].push_back(rr[i]); vals[2].push_back(vr[i] % P);
+    vals[3].push_back(mulmod(sec[i], rr[i])); vals[4].push_back(mulmod(vr[i] % P, rr[i]));
+  }
+  Bytes parts[2][5];
+  for (int k = 0; k < 5; ++k) {
+    std::vector<u128> a(W), b(W);
+    for (size_t i = 0; i < W; ++i) {
+      a[i] = ((u128)rng() << 64 | rng()) % P;
+      b[i] = vals[k][i] >= a[i] ? vals[k][i] - a[i] : vals[k][i] + (P - a[i]);
+    }
+    parts[0][k] = c.toGfp(a);
+    parts[1][k] = c.toGfp(b);
+  }
+  std::vector<OutputDeliveryObject> odos;
+  for (int j = 0; j < 2; ++j)
+    odos.emplace_back(parts[j][0], parts[j][1], parts[j][2], parts[j][3], parts[j][4]);
+  EXPECT(client::verifyOutputDeliveryObjects(util, odos) == sec);
+  // masking with these as Input Mask ODOs: masked + mask == secret
+  std::vector<u128> secrets(W);
+  for (auto& x : secrets) x = rng();
+  auto maskedWords = client::maskSecret(util, secrets, odos);
+  for (size_t i = 0; i < W; i += 97) {
+    const u128 mv = c.fromGfp(maskedWords[i])[0];
+    EXPECT(addMod(mv, sec[i], P) == secrets[i] % P);
+  }
+  // tamper party 1's w share of word 5 -> IntegrityVerificationException
+  Bytes wt = parts[1][3];
+  wt[16 * 5] ^= 1;
+  std::vector<OutputDeliveryObject> bad = {odos[0], OutputDeliveryObject(parts[1][0], parts[1][1], parts[1][2], wt, parts[1][4])};
+  threw = false;
+  try {
+    client::verifyOutputDeliveryObjects(util, bad);
+  } catch (const IntegrityVerificationException&) {
+    threw = true;
+  }
+  EXPECT(threw);
+}
+
+int main(int argc, char** argv) {
+  const std::string mode = argc > 1 ? argv[1] : "cpu";
+  try {
+    cpu_tests();
+    if (mode == "gpu") gpu_tests();
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "exception: %s\n", e.what());
+    return 2;
+  }
+  std::printf("%s: %d failures\n", mode.c_str(), failures);
+  return failures ? 1 : 0;
+}

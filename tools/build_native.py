@@ -51,5 +51,25 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+CPP_TEST_SRC = os.path.join(ROOT, "tests", "cpp", "mirror_test.cpp")
+CPP_TEST_BIN = os.path.join(ROOT, "tests", "cpp", "mirror_test")
+
+
+def build_cpp_test(force: bool = False) -> str:
+    """The C++ host-mirror test program (include/amphora.hpp) against the .so."""
+    deps = [CPP_TEST_SRC, os.path.join(ROOT, "include", "amphora.hpp"), LIB]
+    if not force and os.path.exists(CPP_TEST_BIN) and all(
+            os.path.getmtime(d) <= os.path.getmtime(CPP_TEST_BIN) for d in deps):
+        return CPP_TEST_BIN
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-I" + os.path.join(ROOT, "include"), CPP_TEST_SRC,
+           "-L" + HERE, "-lamphora_hip", "-Wl,-rpath,$ORIGIN/../../amphora_amd", "-o", CPP_TEST_BIN]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("g++ failed building the C++ mirror test")
+    return CPP_TEST_BIN
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_cpp_test(force="--force" in sys.argv))
