@@ -73,6 +73,10 @@ def _load():
     L.amph_host_register.argtypes = [vp, vp, sz]
     L.amph_host_unregister.argtypes = [vp, vp]
     L.amph_time_next_launch.argtypes = [vp, vp]
+    L.amph_base64_encode.argtypes = [vp, vp, sz, vp, u32, vp]
+    L.amph_base64_decode.argtypes = [vp, vp, sz, vp, C.POINTER(C.c_size_t), i64p, u32, vp]
+    L.amph_base64_encode_words.argtypes = [vp, vp, sz, vp, u32, vp]
+    L.amph_base64_decode_words.argtypes = [vp, vp, sz, vp, i64p, u32, vp]
     L.amph_synth_odos.argtypes = [vp, u64, i32, sz, C.POINTER(vp), vp, C.c_int64, i32, vp]
     L.amph_synth_words.argtypes = [vp, u64, sz, vp, vp]
     return L
@@ -86,7 +90,8 @@ EXPORTED = ["amph_ctx_create", "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_
             "amph_mask_words", "amph_to_gfp", "amph_from_gfp", "amph_convert_share",
             "amph_odo_pre", "amph_open_diffs", "amph_odo_post", "amph_synth_odos",
             "amph_synth_words", "amph_host_register", "amph_host_unregister",
-            "amph_time_next_launch"]
+            "amph_time_next_launch", "amph_base64_encode", "amph_base64_decode",
+            "amph_base64_encode_words", "amph_base64_decode_words"]
 
 
 class _AmphOdo(C.Structure):
@@ -308,6 +313,55 @@ class Context:
         self._check(lib.amph_odo_post(self._h, _ptr(op), _ptr(tr), W, int(is_player0), _ptr(w),
                                       _ptr(u), flags, stream))
         return w, u
+
+    # -- wire codec (base64 as Jackson writes byte[]) ---------------------------
+    def base64_encode(self, data) -> bytes:
+        """bytes / uint8 array -> base64 ASCII (bytes); device tensor -> device tensor."""
+        a = data if _is_dev(data) else np.frombuffer(bytes(data), np.uint8) \
+            if isinstance(data, (bytes, bytearray, memoryview)) else np.ascontiguousarray(data, np.uint8).reshape(-1)
+        n = a.numel() if _is_dev(a) else a.size
+        flags, stream = self._mode(a)
+        out = self._empty(a, (4 * ((n + 2) // 3),))
+        self._check(lib.amph_base64_encode(self._h, _ptr(a), n, _ptr(out), flags, stream))
+        return out if _is_dev(a) else out.tobytes()
+
+    def base64_decode(self, text) -> bytes:
+        """base64 ASCII (str / bytes / uint8 array) -> bytes; raises ValueError on
+        an illegal character or a length not divisible by 4."""
+        if isinstance(text, str):
+            text = text.encode("ascii", errors="replace")
+        a = text if _is_dev(text) else np.frombuffer(bytes(text), np.uint8) \
+            if isinstance(text, (bytes, bytearray, memoryview)) else np.ascontiguousarray(text, np.uint8).reshape(-1)
+        n = a.numel() if _is_dev(a) else a.size
+        flags, stream = self._mode(a)
+        out = self._empty(a, (3 * n // 4,))
+        ob = C.c_size_t(0)
+        bad, badp = self._ff(a)
+        st = lib.amph_base64_decode(self._h, _ptr(a), n, _ptr(out), C.byref(ob), badp, flags, stream)
+        if st in (AMPH_E_PARAM, AMPH_E_LEN):
+            raise ValueError(lib.amph_last_error().decode())
+        self._check(st)
+        if _is_dev(a):
+            return out[: ob.value], bad
+        return out[: ob.value].tobytes()
+
+    def base64_encode_words(self, words16):
+        w = words_view(words16)
+        flags, stream = self._mode(w)
+        out = self._empty(w, (w.shape[0], 24))
+        self._check(lib.amph_base64_encode_words(self._h, _ptr(w), w.shape[0], _ptr(out), flags, stream))
+        return out
+
+    def base64_decode_words(self, records24):
+        r = words_view(records24, 24)
+        flags, stream = self._mode(r)
+        out = self._empty(r, (r.shape[0], 16))
+        bad, badp = self._ff(r)
+        st = lib.amph_base64_decode_words(self._h, _ptr(r), r.shape[0], _ptr(out), badp, flags, stream)
+        if st == AMPH_E_PARAM and not _is_dev(r):
+            raise ValueError(lib.amph_last_error().decode())
+        self._check(st)
+        return out if not _is_dev(r) else (out, bad)
 
     # -- synthetic device inputs (bench / tests) --------------------------------
     def synth_odos(self, seed: int, n: int, words: int, fault_index: int = -1,

@@ -117,6 +117,7 @@ struct amph_ctx {
   hipStream_t streams[kSlots] = {};
   Slot slots[kSlots];
   DevBuf ff;  // per-batch first-fail words (host path)
+  DevBuf tail;  // small scratch for the partial last unit of codec calls
   std::unique_ptr<amph::CopyPool> pool;
 };
 
@@ -421,6 +422,7 @@ void amph_ctx_destroy(amph_ctx* c) {
       if (c->streams[s]) (void)hipStreamDestroy(c->streams[s]);
     }
     c->ff.release();
+    c->tail.release();
   }
   delete c;
 }
@@ -747,6 +749,154 @@ int amph_mask_words(amph_ctx* c, const uint8_t* secrets, const uint8_t* masks, s
                          const amph::LaunchCfg& lc) {
                        return amph::launch_mask_words(din[0], din[1], cnt, dout[0], c->f, lc);
                      });
+}
+
+// ---- base64 wire codec ---------------------------------------------------------
+}  // extern "C"
+namespace {
+size_t b64_padding(const char* last2) {
+  return (last2[1] == '=') + (last2[1] == '=' && last2[0] == '=');
+}
+
+// Host-path helper for the < 1-unit tail: copy in, run, copy out, synchronously.
+template <class Launch>
+int run_tail(amph_ctx* c, const void* in, size_t in_bytes, void* out, size_t out_bytes,
+             bool with_bad, unsigned long long* bad_host, Launch&& launch) {
+  HIP_TRY(hipSetDevice(c->device));
+  hipError_t e = c->tail.ensure(512);
+  if (e != hipSuccess) return fail(AMPH_E_NOMEM, "tail scratch");
+  uint8_t* d = (uint8_t*)c->tail.p;
+  HIP_TRY(hipMemcpy(d, in, in_bytes, hipMemcpyHostToDevice));
+  if (with_bad) HIP_TRY(hipMemset(d + 448, 0x7F, 8));
+  e = launch(d, d + 256, (unsigned long long*)(d + 448), cfg(c, nullptr, 1));
+  if (e != hipSuccess) return hip_fail(e, "codec tail");
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, d + 256, out_bytes, hipMemcpyDeviceToHost));
+  if (with_bad) HIP_TRY(hipMemcpy(bad_host, d + 448, 8, hipMemcpyDeviceToHost));
+  return AMPH_OK;
+}
+}  // namespace
+extern "C" {
+
+int amph_base64_encode(amph_ctx* c, const uint8_t* in, size_t nbytes, char* out, uint32_t flags,
+                       void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (nbytes && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
+  if (flags & AMPH_F_DEVICE) {
+    HIP_TRY(hipSetDevice(c->device));
+    hipError_t e = amph::launch_b64_encode(in, nbytes, out, cfg(c, (hipStream_t)stream, (nbytes + 11) / 12));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_b64_encode");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  const size_t units = nbytes / 12, rem = nbytes % 12;
+  int st = run_batched(c, units, {{in, 12}}, {{(uint8_t*)out, 16}}, false, nullptr,
+                       [&](auto& din, auto& dout, size_t cnt, unsigned long long*,
+                           const amph::LaunchCfg& lc) {
+                         return amph::launch_b64_encode((const uint8_t*)din[0], 12 * cnt,
+                                                        (char*)dout[0], lc);
+                       });
+  if (st != AMPH_OK || rem == 0) return st;
+  return run_tail(c, in + 12 * units, rem, out + 16 * units, 4 * ((rem + 2) / 3), false, nullptr,
+                  [&](uint8_t* di, uint8_t* dout, unsigned long long*, const amph::LaunchCfg& lc) {
+                    return amph::launch_b64_encode(di, rem, (char*)dout, lc);
+                  });
+}
+
+int amph_base64_decode(amph_ctx* c, const char* in, size_t nchars, uint8_t* out,
+                       size_t* out_bytes, int64_t* bad_index, uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (nchars % 4) return fail(AMPH_E_LEN, "base64 input length must be a multiple of 4");
+  if (nchars && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
+  if (bad_index && !(flags & AMPH_F_DEVICE)) *bad_index = -1;
+  if (nchars == 0) {
+    if (out_bytes) *out_bytes = 0;
+    return AMPH_OK;
+  }
+  char last2[2];
+  if (flags & AMPH_F_DEVICE) {
+    HIP_TRY(hipSetDevice(c->device));
+    if (!bad_index) return fail(AMPH_E_PARAM, "bad_index is required");
+    // one 2-byte read-back decides the padding (the only synchronous step)
+    HIP_TRY(hipMemcpyAsync(last2, in + nchars - 2, 2, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    const size_t ob = 3 * nchars / 4 - b64_padding(last2);
+    if (out_bytes) *out_bytes = ob;
+    if (int st = reset_ff_dev(bad_index, flags, (hipStream_t)stream)) return st;
+    hipError_t e = amph::launch_b64_decode(in, nchars, out, ob, (unsigned long long*)bad_index,
+                                           cfg(c, (hipStream_t)stream, (nchars + 15) / 16));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_b64_decode");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  std::memcpy(last2, in + nchars - 2, 2);
+  const size_t ob = 3 * nchars / 4 - b64_padding(last2);
+  if (out_bytes) *out_bytes = ob;
+  // full 16-char units that contain no padding go through the batched path
+  const size_t units = (nchars - 4) / 16, tail_chars = nchars - 16 * units;
+  int64_t bad = -1;
+  int st = run_batched(c, units, {{(const uint8_t*)in, 16}}, {{out, 12}}, true, &bad,
+                       [&](auto& din, auto& dout, size_t cnt, unsigned long long* ff,
+                           const amph::LaunchCfg& lc) {
+                         return amph::launch_b64_decode((const char*)din[0], 16 * cnt,
+                                                        (uint8_t*)dout[0], 12 * cnt, ff, lc);
+                       });
+  if (st != AMPH_OK && st != AMPH_E_VERIFY) return st;
+  unsigned long long tb = amph::kNoFail;
+  const size_t tail_out = ob - 12 * units;
+  int st2 = run_tail(c, in + 16 * units, tail_chars, out + 12 * units, tail_out, true, &tb,
+                     [&](uint8_t* di, uint8_t* dout, unsigned long long* bb, const amph::LaunchCfg& lc) {
+                       return amph::launch_b64_decode((const char*)di, tail_chars, dout, tail_out,
+                                                      bb, lc);
+                     });
+  if (st2 != AMPH_OK) return st2;
+  // the tail kernel saw the tail as the whole text, so its '=' rule is exact
+  const int64_t first = st == AMPH_E_VERIFY ? bad : (tb != amph::kNoFail ? (int64_t)(16 * units + tb) : -1);
+  if (first >= 0) {
+    if (bad_index) *bad_index = first;
+    return fail(AMPH_E_PARAM, "Illegal base64 character at index " + std::to_string(first));
+  }
+  return AMPH_OK;
+}
+
+int amph_base64_encode_words(amph_ctx* c, const uint8_t* words16, size_t words, char* out24,
+                             uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (words && (!words16 || !out24)) return fail(AMPH_E_PARAM, "null buffer");
+  if (flags & AMPH_F_DEVICE) {
+    HIP_TRY(hipSetDevice(c->device));
+    hipError_t e = amph::launch_b64_words((const uint4*)words16, words, out24, cfg(c, (hipStream_t)stream, words));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_b64_words");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  return run_batched(c, words, {{words16, 16}}, {{(uint8_t*)out24, 24}}, false, nullptr,
+                     [&](auto& din, auto& dout, size_t cnt, unsigned long long*,
+                         const amph::LaunchCfg& lc) {
+                       return amph::launch_b64_words(din[0], cnt, (char*)dout[0], lc);
+                     });
+}
+
+int amph_base64_decode_words(amph_ctx* c, const char* in24, size_t words, uint8_t* out16,
+                             int64_t* bad_index, uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (words && (!in24 || !out16)) return fail(AMPH_E_PARAM, "null buffer");
+  if (flags & AMPH_F_DEVICE) {
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipSetDevice(c->device));
+    if (int st = reset_ff_dev(bad_index, flags, s)) return st;
+    hipError_t e = amph::launch_b64_unwords(in24, words, (uint4*)out16, (unsigned long long*)bad_index,
+                                            cfg(c, s, words));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_b64_unwords");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  int64_t bad = -1;
+  int st = run_batched(c, words, {{(const uint8_t*)in24, 24}}, {{out16, 16}}, true, &bad,
+                       [&](auto& din, auto& dout, size_t cnt, unsigned long long* ff,
+                           const amph::LaunchCfg& lc) {
+                         return amph::launch_b64_unwords((const char*)din[0], cnt, dout[0], ff, lc);
+                       });
+  if (bad_index) *bad_index = bad;
+  if (st == AMPH_E_VERIFY)
+    return fail(AMPH_E_PARAM, "Illegal base64 word record at index " + std::to_string(bad));
+  return st;
 }
 
 int amph_host_register(amph_ctx* c, void* ptr, size_t bytes) {

@@ -1,0 +1,232 @@
+// Base64 wire codec kernels (gfx950) -- the step either side of the path
+// (SURVEY.md 8f rank 2): the reference ships every share array as base64 in
+// JSON (Jackson's default Base64Variants.MIME_NO_LINEFEEDS: standard
+// alphabet, '=' padding, no line breaks; VerifiableSecretTest.java:41-90) and
+// each masked word as {"value": base64(16 bytes)} (MaskedInputData.java:44-52).
+//
+//   k_b64_encode   byte stream -> chars, one 12-byte unit (16 chars) per lane
+//   k_b64_decode   chars -> byte stream, one 16-char unit per lane, reports the
+//                  first invalid character index
+//   k_b64_words    16-byte words -> 24 chars each (per-word base64, "xx..x==")
+//   k_b64_unwords  24-char records -> 16-byte words
+//
+// Pure byte work, HBM-bound; character mapping is branch-free arithmetic.
+#include <hip/hip_ext.h>
+
+#include "kernels.hpp"
+
+namespace amph {
+
+#define AMPH_LAUNCH(K, G, B, C, ...) \
+  hipExtLaunchKernelGGL(K, G, B, 0, (C).stream, (C).ev_start, (C).ev_stop, 0, __VA_ARGS__)
+
+namespace {
+
+__device__ __forceinline__ uint32_t enc6(uint32_t v) {  // 0..63 -> ASCII
+  return v + 65u + 6u * (v >= 26u) - 75u * (v >= 52u) - 15u * (v >= 62u) + 3u * (v >= 63u);
+}
+
+// ASCII -> 0..63, or 0xFF if not in the alphabet
+__device__ __forceinline__ uint32_t dec6(uint32_t c) {
+  uint32_t v = 0xFFu;
+  v = (c >= 'A' && c <= 'Z') ? c - 'A' : v;
+  v = (c >= 'a' && c <= 'z') ? c - 'a' + 26u : v;
+  v = (c >= '0' && c <= '9') ? c - '0' + 52u : v;
+  v = c == '+' ? 62u : v;
+  v = c == '/' ? 63u : v;
+  return v;
+}
+
+// 3 bytes (big-endian group) -> 4 chars packed little-endian in a uint32
+__device__ __forceinline__ uint32_t enc_group(uint32_t b0, uint32_t b1, uint32_t b2) {
+  const uint32_t g = (b0 << 16) | (b1 << 8) | b2;
+  return enc6((g >> 18) & 63u) | (enc6((g >> 12) & 63u) << 8) | (enc6((g >> 6) & 63u) << 16) |
+         (enc6(g & 63u) << 24);
+}
+
+__global__ __launch_bounds__(kMaxBlock) void k_b64_encode(const uint8_t* in, size_t nbytes,
+                                                      char* out) {
+  const size_t units = (nbytes + 11) / 12;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < units; t += stride) {
+    const size_t base = 12 * t;
+    const size_t rem = nbytes - base < 12 ? nbytes - base : 12;
+    uint8_t b[12];
+    if (rem == 12 && (((uintptr_t)(in + base)) & 3) == 0) {
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(in + base);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const uint32_t x = __builtin_nontemporal_load(w + q);
+        b[4 * q] = x & 0xFF; b[4 * q + 1] = (x >> 8) & 0xFF;
+        b[4 * q + 2] = (x >> 16) & 0xFF; b[4 * q + 3] = x >> 24;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 12; ++q) b[q] = (size_t)q < rem ? in[base + q] : 0;
+    }
+    uint32_t g[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) g[q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
+    char* o = out + 16 * t;
+    if (rem == 12 && (((uintptr_t)o) & 15) == 0) {
+      *reinterpret_cast<uint4*>(o) = make_uint4(g[0], g[1], g[2], g[3]);
+    } else {
+      // final partial unit: ceil(rem / 3) groups, '=' for the missing bytes
+      const int groups = (int)((rem + 2) / 3);
+      for (int q = 0; q < groups; ++q) {
+        const int have = (int)rem - 3 * q;  // bytes present in this group (1..3)
+        for (int k = 0; k < 4; ++k) {
+          char ch = (char)((g[q] >> (8 * k)) & 0xFF);
+          if (k >= 2 && have < k) ch = '=';
+          o[4 * q + k] = ch;
+        }
+      }
+    }
+  }
+}
+
+// nchars % 4 == 0; out_bytes = 3 nchars / 4 - padding; bad = first invalid index
+__global__ __launch_bounds__(kMaxBlock) void k_b64_decode(const char* in, size_t nchars,
+                                                      uint8_t* out, size_t out_bytes,
+                                                      unsigned long long* bad) {
+  const size_t units = (nchars + 15) / 16;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < units; t += stride) {
+    const size_t base = 16 * t;
+    const size_t rem = nchars - base < 16 ? nchars - base : 16;
+    uint8_t c[16];
+    if (rem == 16 && (((uintptr_t)(in + base)) & 15) == 0) {
+      const uint4 v = *reinterpret_cast<const uint4*>(in + base);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 16; ++q) c[q] = (w[q >> 2] >> (8 * (q & 3))) & 0xFF;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) c[q] = (size_t)q < rem ? (uint8_t)in[base + q] : 'A';
+    }
+    uint32_t firstbad = 0xFFFFFFFFu;
+    uint8_t o[12];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const size_t pos = base + 4 * q + k;
+        // '=' is legal only in the last two positions of the whole text
+        const bool pad_ok = c[4 * q + k] == '=' && pos >= nchars - 2 &&
+                            (pos == nchars - 1 || in[nchars - 1] == '=');
+        v[k] = pad_ok ? 0u : dec6(c[4 * q + k]);
+        if (v[k] == 0xFFu && firstbad == 0xFFFFFFFFu) firstbad = (uint32_t)(4 * q + k);
+      }
+      const uint32_t g = (v[0] << 18) | (v[1] << 12) | (v[2] << 6) | v[3];
+      o[3 * q] = (g >> 16) & 0xFF;
+      o[3 * q + 1] = (g >> 8) & 0xFF;
+      o[3 * q + 2] = g & 0xFF;
+    }
+    if (firstbad != 0xFFFFFFFFu && (size_t)firstbad < rem) atomicMin(bad, (unsigned long long)(base + firstbad));
+    const size_t ob = 12 * t;
+    uint8_t* op = out + ob;
+    if (ob + 12 <= out_bytes && (((uintptr_t)op) & 3) == 0) {
+      uint32_t* w = reinterpret_cast<uint32_t*>(op);
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        w[q] = o[4 * q] | (o[4 * q + 1] << 8) | (o[4 * q + 2] << 16) | ((uint32_t)o[4 * q + 3] << 24);
+    } else {
+      for (int q = 0; q < 12; ++q)
+        if (ob + q < out_bytes) op[q] = o[q];
+    }
+  }
+}
+
+// 16-byte word -> 24 chars ("...==": 5 full groups + 1 byte)
+__global__ __launch_bounds__(kMaxBlock) void k_b64_words(const uint4* in, size_t words, char* out) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
+    const uint4 v = in[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint8_t b[18];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) b[q] = (w[q >> 2] >> (8 * (q & 3))) & 0xFF;
+    b[16] = b[17] = 0;
+    uint32_t g[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) g[q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
+    g[5] = (g[5] & 0xFFFFu) | ((uint32_t)'=' << 16) | ((uint32_t)'=' << 24);
+    uint2* o = reinterpret_cast<uint2*>(out + 24 * i);  // 8-byte aligned when out is
+    o[0] = make_uint2(g[0], g[1]);
+    o[1] = make_uint2(g[2], g[3]);
+    o[2] = make_uint2(g[4], g[5]);
+  }
+}
+
+// 24-char records -> 16-byte words; bad = first invalid record index
+__global__ __launch_bounds__(kMaxBlock) void k_b64_unwords(const char* in, size_t words, uint4* out,
+                                                       unsigned long long* bad) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
+    const uint2* p = reinterpret_cast<const uint2*>(in + 24 * i);
+    const uint2 x0 = p[0], x1 = p[1], x2 = p[2];
+    const uint32_t w[6] = {x0.x, x0.y, x1.x, x1.y, x2.x, x2.y};
+    uint8_t b[18];
+    bool ok = ((w[5] >> 16) & 0xFF) == '=' && (w[5] >> 24) == '=';
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t ch = (w[q] >> (8 * k)) & 0xFF;
+        v[k] = (q == 5 && k >= 2) ? 0u : dec6(ch);
+        ok &= v[k] != 0xFFu;
+      }
+      const uint32_t g = (v[0] << 18) | (v[1] << 12) | (v[2] << 6) | v[3];
+      b[3 * q] = (g >> 16) & 0xFF;
+      b[3 * q + 1] = (g >> 8) & 0xFF;
+      b[3 * q + 2] = g & 0xFF;
+    }
+    // like java.util.Base64 / Jackson, the unused low bits of the last group are ignored
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      o[q] = b[4 * q] | (b[4 * q + 1] << 8) | (b[4 * q + 2] << 16) | ((uint32_t)b[4 * q + 3] << 24);
+    out[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    if (!ok) atomicMin(bad, (unsigned long long)i);
+  }
+}
+
+unsigned grid_n(size_t n, const LaunchCfg& c) {
+  size_t g = (n + c.block - 1) / c.block;
+  if (c.grid_cap > 0 && g > (size_t)c.grid_cap) g = (size_t)c.grid_cap;
+  if (g > 0x7FFFFFFFu) g = 0x7FFFFFFFu;
+  return (unsigned)(g ? g : 1);
+}
+
+}  // namespace
+
+hipError_t launch_b64_encode(const uint8_t* in, size_t nbytes, char* out, const LaunchCfg& c) {
+  if (nbytes == 0) return hipSuccess;
+  AMPH_LAUNCH(k_b64_encode, dim3(grid_n((nbytes + 11) / 12, c)), dim3(c.block), c, in, nbytes, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_b64_decode(const char* in, size_t nchars, uint8_t* out, size_t out_bytes,
+                             unsigned long long* bad, const LaunchCfg& c) {
+  if (nchars == 0) return hipSuccess;
+  AMPH_LAUNCH(k_b64_decode, dim3(grid_n((nchars + 15) / 16, c)), dim3(c.block), c, in, nchars, out,
+              out_bytes, bad);
+  return hipGetLastError();
+}
+
+hipError_t launch_b64_words(const uint4* in, size_t words, char* out, const LaunchCfg& c) {
+  if (words == 0) return hipSuccess;
+  AMPH_LAUNCH(k_b64_words, dim3(grid_n(words, c)), dim3(c.block), c, in, words, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_b64_unwords(const char* in, size_t words, uint4* out, unsigned long long* bad,
+                              const LaunchCfg& c) {
+  if (words == 0) return hipSuccess;
+  AMPH_LAUNCH(k_b64_unwords, dim3(grid_n(words, c)), dim3(c.block), c, in, words, out, bad);
+  return hipGetLastError();
+}
+
+}  // namespace amph

@@ -82,6 +82,14 @@ hipError_t launch_from_gfp(const uint4* in, size_t words, uint4* out, const Fp& 
 hipError_t launch_mask_words(const uint4* secrets, const uint4* masks, size_t words, uint4* out,
                              const Fp& f, const LaunchCfg& c);
 
+// base64 wire codec (codec.hip): standard alphabet, '=' padding, no line breaks.
+hipError_t launch_b64_encode(const uint8_t* in, size_t nbytes, char* out, const LaunchCfg& c);
+hipError_t launch_b64_decode(const char* in, size_t nchars, uint8_t* out, size_t out_bytes,
+                             unsigned long long* bad, const LaunchCfg& c);
+hipError_t launch_b64_words(const uint4* in, size_t words, char* out, const LaunchCfg& c);
+hipError_t launch_b64_unwords(const char* in, size_t words, uint4* out, unsigned long long* bad,
+                              const LaunchCfg& c);
+
 // Synthetic honest n-party ODOs (bench/test input generator, device-side).
 struct OutSet {
   uint4* f[5][kMaxParties];

@@ -1,0 +1,160 @@
+"""Wire formats of the hot path's inputs and outputs, with the byte arrays
+base64-coded on the GPU (amph_base64_*).
+
+* VerifiableSecretShare JSON (GET /secret-shares/{id}):
+  amphora-common/.../VerifiableSecretShare.java:30-87 -- the Metadata fields
+  (secretId, tags) followed by the OutputDeliveryObject fields (secretShares,
+  rShares, vShares, wShares, uShares) as base64 strings; pretty form pinned by
+  VerifiableSecretTest.java:41-90 (Jackson's DefaultPrettyPrinter).
+* OutputDeliveryObject JSON (GET /input-masks): the five base64 fields.
+* MaskedInput JSON (POST /masked-inputs): MaskedInput.java:25-62 --
+  {"secretId", "data": [{"value": base64(16 bytes)}, ...], "tags"}; each word
+  is coded on its own (24 chars), the records are framed with numpy.
+
+Large payloads: the base64 spans are located by key with str.find (no JSON
+tree is built for them); only the small remainder goes through json.loads.
+"""
+from __future__ import annotations
+
+import json
+import uuid
+from typing import List, Tuple
+
+import numpy as np
+
+from . import _lib
+from .entities import (IllegalArgumentException, MaskedInput, MaskedInputData,
+                       OutputDeliveryObject)
+
+ODO_FIELDS = ("secretShares", "rShares", "vShares", "wShares", "uShares")
+
+
+def _tag_obj(t):
+    if isinstance(t, dict):
+        d = dict(t)
+    else:
+        k, v = t[0], t[1]
+        d = {"key": k, "value": v, "valueType": t[2] if len(t) > 2 else "STRING"}
+    d.setdefault("valueType", "STRING")
+    return {"key": d["key"], "value": d["value"], "valueType": d["valueType"]}
+
+
+def _pretty_tags(tags, indent="  "):
+    if not tags:
+        return "[ ]"
+    items = []
+    for t in tags:
+        o = _tag_obj(t)
+        items.append("{\n" + ",\n".join('%s  "%s" : %s' % (indent, k, json.dumps(o[k])) for k in o)
+                     + "\n" + indent + "}")
+    return "[ " + ", ".join(items) + " ]"
+
+
+def vss_to_json(ctx: _lib.Context, secret_id: uuid.UUID, tags, odo: OutputDeliveryObject,
+                pretty: bool = True) -> str:
+    """VerifiableSecretShare -> JSON (Jackson's pretty printer layout when pretty)."""
+    b64 = [ctx.base64_encode(bytes(f)).decode("ascii") for f in odo.fields()]
+    if pretty:
+        lines = ['  "secretId" : "%s"' % secret_id, '  "tags" : %s' % _pretty_tags(tags)]
+        lines += ['  "%s" : "%s"' % (k, v) for k, v in zip(ODO_FIELDS, b64)]
+        return "{\n" + ",\n".join(lines) + "\n}"
+    head = {"secretId": str(secret_id), "tags": [_tag_obj(t) for t in tags]}
+    body = ",".join('"%s":"%s"' % (k, v) for k, v in zip(ODO_FIELDS, b64))
+    return json.dumps(head, separators=(",", ":"))[:-1] + "," + body + "}"
+
+
+def odo_to_json(ctx: _lib.Context, odo: OutputDeliveryObject) -> str:
+    b64 = [ctx.base64_encode(bytes(f)).decode("ascii") for f in odo.fields()]
+    return "{" + ",".join('"%s":"%s"' % (k, v) for k, v in zip(ODO_FIELDS, b64)) + "}"
+
+
+def _extract(text: str, key: str) -> Tuple[str, int, int]:
+    """Locate "key" : "<value>" and return (value, start, end) of the quoted span."""
+    pat = '"%s"' % key
+    i = text.find(pat)
+    if i < 0:
+        return None, -1, -1
+    j = i + len(pat)
+    while text[j] in " \t\r\n":
+        j += 1
+    if text[j] != ":":
+        raise ValueError("malformed JSON near %s" % key)
+    j += 1
+    while text[j] in " \t\r\n":
+        j += 1
+    if text.startswith("null", j):
+        return None, i, j + 4
+    if text[j] != '"':
+        raise ValueError("field %s is not a string" % key)
+    k = text.find('"', j + 1)
+    return text[j + 1:k], i, k + 1
+
+
+def _odo_from_text(ctx: _lib.Context, text: str):
+    vals, spans = [], []
+    for k in ODO_FIELDS:
+        v, s, e = _extract(text, k)
+        if v is None:
+            # Lombok @NonNull through Jackson's ValueInstantiationException
+            raise IllegalArgumentException("%s is marked non-null but is null" % k)
+        vals.append(ctx.base64_decode(v))
+        spans.append((s, e))
+    return OutputDeliveryObject(*vals), spans
+
+
+def odo_from_json(ctx: _lib.Context, text: str) -> OutputDeliveryObject:
+    return _odo_from_text(ctx, text)[0]
+
+
+def vss_from_json(ctx: _lib.Context, text: str):
+    """JSON -> (secret_id, tags, OutputDeliveryObject); unknown fields ignored
+    (VSSDeserializer: FAIL_ON_UNKNOWN_PROPERTIES disabled)."""
+    odo, spans = _odo_from_text(ctx, text)
+    rest, pos = [], 0
+    for s, e in sorted(spans):
+        rest.append(text[pos:s])
+        pos = e
+        # drop the separating comma that followed the removed member, if any
+        while pos < len(text) and text[pos] in " \t\r\n":
+            pos += 1
+        if pos < len(text) and text[pos] == ",":
+            pos += 1
+    rest.append(text[pos:])
+    small = "".join(rest).strip()
+    small = small.replace(",}", "}").replace(",\n}", "\n}")
+    meta = json.loads(small) if small else {}
+    if meta.get("secretId") is None:
+        raise IllegalArgumentException("secretId is marked non-null but is null")
+    return uuid.UUID(meta["secretId"]), list(meta.get("tags") or []), odo
+
+
+def masked_input_to_json(ctx: _lib.Context, mi: MaskedInput) -> str:
+    """MaskedInput -> compact JSON; the per-word base64 runs on the GPU and
+    the {"value":"..."} records are framed with numpy (37 B per word)."""
+    W = len(mi.data)
+    if W:
+        words = np.frombuffer(b"".join(d.value for d in mi.data), np.uint8).reshape(W, 16)
+        rec = ctx.base64_encode_words(words)
+        frame = np.empty((W, 37), np.uint8)
+        frame[:, :10] = np.frombuffer(b'{"value":"', np.uint8)
+        frame[:, 10:34] = rec
+        frame[:, 34:37] = np.frombuffer(b'"},', np.uint8)
+        data = b"[" + frame.tobytes()[:-1] + b"]"
+    else:
+        data = b"[]"
+    tags = json.dumps([_tag_obj(t) for t in mi.tags], separators=(",", ":"))
+    return '{"secretId":"%s","data":%s,"tags":%s}' % (mi.secret_id, data.decode("ascii"), tags)
+
+
+def masked_input_from_json(ctx: _lib.Context, text: str) -> MaskedInput:
+    obj = json.loads(text)
+    if obj.get("secretId") is None:
+        raise IllegalArgumentException("secretId is marked non-null but is null")
+    values = [d["value"] for d in (obj.get("data") or [])]
+    if values and all(isinstance(v, str) and len(v) == 24 for v in values):
+        rec = np.frombuffer("".join(values).encode("ascii"), np.uint8).reshape(-1, 24)
+        words = ctx.base64_decode_words(rec)
+        data = [MaskedInputData.of(bytes(w)) for w in words]
+    else:  # MaskedInputData.of enforces the 16-byte length with the reference message
+        data = [MaskedInputData.of(ctx.base64_decode(v)) for v in values]
+    return MaskedInput(uuid.UUID(obj["secretId"]), data, list(obj.get("tags") or []))

@@ -215,6 +215,27 @@ int amph_open_diffs(amph_ctx* ctx, const uint8_t* const* diff_mags,
 int amph_odo_post(amph_ctx* ctx, const uint8_t* opened, const uint8_t* triples, size_t words,
                   int is_player0, uint8_t* out_w, uint8_t* out_u, uint32_t flags, void* stream);
 
+/* ---- wire codec ----------------------------------
+ * Base64 as Jackson writes byte[] (Base64Variants.MIME_NO_LINEFEEDS: standard
+ * alphabet, '=' padding, no line breaks): the secretShares/rShares/... fields
+ * of VerifiableSecretShare / OutputDeliveryObject JSON
+ * (amphora-common/.../VerifiableSecretTest.java:41-90) and the per-word
+ * {"value": ...} of MaskedInputData (MaskedInputData.java:44-52).
+ * encode: out gets 4 * ceil(nbytes / 3) chars.
+ * decode: nchars % 4 == 0 (else AMPH_E_LEN); *out_bytes = decoded length;
+ *   an illegal character returns AMPH_E_PARAM with *bad_index = its position
+ *   (device mode: bad_index is a device word, AMPH_NO_FAILURE if clean; the
+ *   call reads the last 2 chars back to size the output).
+ * words: one 16-byte word <-> one 24-char record (per-word base64). */
+int amph_base64_encode(amph_ctx* ctx, const uint8_t* in, size_t nbytes, char* out, uint32_t flags,
+                       void* stream);
+int amph_base64_decode(amph_ctx* ctx, const char* in, size_t nchars, uint8_t* out,
+                       size_t* out_bytes, int64_t* bad_index, uint32_t flags, void* stream);
+int amph_base64_encode_words(amph_ctx* ctx, const uint8_t* words16, size_t words, char* out24,
+                             uint32_t flags, void* stream);
+int amph_base64_decode_words(amph_ctx* ctx, const char* in24, size_t words, uint8_t* out16,
+                             int64_t* bad_index, uint32_t flags, void* stream);
+
 /* ---- benchmark / test input generation (device pointers only) ---------- */
 /* Honest n-party ODOs: out_fields[k * n_parties + j] = field k (y,r,v,w,u) of
  * party j (device, words x 16 B each).  out_plain_y (optional, device) gets the
