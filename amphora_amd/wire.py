@@ -17,6 +17,7 @@ tree is built for them); only the small remainder goes through json.loads.
 from __future__ import annotations
 
 import json
+import re
 import uuid
 from typing import List, Tuple
 
@@ -120,8 +121,7 @@ def vss_from_json(ctx: _lib.Context, text: str):
         if pos < len(text) and text[pos] == ",":
             pos += 1
     rest.append(text[pos:])
-    small = "".join(rest).strip()
-    small = small.replace(",}", "}").replace(",\n}", "\n}")
+    small = re.sub(r",\s*}\s*$", "}", "".join(rest).strip())
     meta = json.loads(small) if small else {}
     if meta.get("secretId") is None:
         raise IllegalArgumentException("secretId is marked non-null but is null")
