@@ -179,6 +179,34 @@ def test_host_stream_pinned_and_pageable(ctx, F):
     assert np.array_equal(y1, oy) and np.array_equal(y2, oy) and np.array_equal(m2, om)
 
 
+def test_concurrent_callers(ctx, F):
+    """Host-path calls from several threads (ctypes releases the GIL): one
+    shared context (calls serialise on its lock) and a second context of its
+    own; every result matches the oracle, faults stay with their caller."""
+    import threading
+    import amphora_amd as A
+    ctx2 = A.Context(P, R, RINV, device=0)
+    cases = []
+    for t in range(6):
+        odos, _ = F.synth_odos(seed=500 + t, n=2 + t % 2, W=20_000 + 777 * t,
+                               fault_index=(1000 * t if t % 3 == 0 else -1))
+        cases.append((odos, F.recombine_verify(odos)))
+    got = [None] * len(cases)
+
+    def work(i):
+        c = ctx2 if i % 2 else ctx
+        for _ in range(3):
+            got[i] = c.recombine_verify(cases[i][0])
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(cases))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for (odos, (oy, off)), (y, ff) in zip(cases, got):
+        assert ff == off and np.array_equal(y, oy)
+
+
 def test_empty_and_single(ctx):
     z = np.zeros((0, 16), np.uint8)
     y, ff = ctx.recombine_verify([(z,) * 5, (z,) * 5])

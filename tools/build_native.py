@@ -70,6 +70,42 @@ def build_cpp_test(force: bool = False) -> str:
     return CPP_TEST_BIN
 
 
+SAN_DIR = os.path.join(ROOT, "build", "sanitize")
+SAN_FLAGS = ["-fsanitize=address", "-fsanitize=undefined", "-fno-sanitize-recover=all",
+             "-fno-omit-frame-pointer"]
+
+
+def build_sanitized(force: bool = False) -> dict:
+    """Host-code ASan/UBSan builds: the library with its
+    host side instrumented (device code untouched -- GPU ASan is not
+    available), the C++ mirror test linked against it, and a driver of the C
+    oracle.  Output in build/sanitize/ (git-ignored)."""
+    os.makedirs(SAN_DIR, exist_ok=True)
+    lib = os.path.join(SAN_DIR, "libamphora_hip.so")
+    mirror = os.path.join(SAN_DIR, "mirror_test")
+    orc = os.path.join(SAN_DIR, "oracle_sanitize")
+    orc_src = os.path.join(ROOT, "tests", "cpp", "oracle_sanitize.c")
+    jobs = [
+        (lib, DEPS, [hipcc(), "--offload-arch=%s" % ARCH, "-O1", "-g", "-std=c++17", "-fPIC", "-shared",
+                     "-mcode-object-version=5", "-I" + os.path.join(ROOT, "include"),
+                     "-Wl,-rpath,/opt/rocm/lib", "-o", lib] + SOURCES
+         + [x for f in SAN_FLAGS for x in ("-Xarch_host", f)]),
+        (mirror, [CPP_TEST_SRC, os.path.join(ROOT, "include", "amphora.hpp"), lib],
+         ["/opt/rocm/llvm/bin/clang++", "-std=c++17", "-O1", "-g", "-I" + os.path.join(ROOT, "include"),
+          CPP_TEST_SRC, "-L" + SAN_DIR, "-lamphora_hip", "-Wl,-rpath,$ORIGIN", "-o", mirror] + SAN_FLAGS),
+        (orc, [orc_src, os.path.join(ROOT, "oracle", "amphora_oracle.c")],
+         ["gcc", "-O1", "-g", "-fopenmp", "-Wall", "-Wextra", orc_src, "-o", orc] + SAN_FLAGS),
+    ]
+    for out, deps, cmd in jobs:
+        if not force and os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
+            continue
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            sys.stderr.write(r.stdout + r.stderr)
+            raise RuntimeError("sanitizer build failed: %s" % out)
+    return {"lib": lib, "mirror": mirror, "oracle": orc}
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
     print(build_cpp_test(force="--force" in sys.argv))
