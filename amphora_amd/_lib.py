@@ -77,6 +77,10 @@ def _load():
     L.amph_base64_decode.argtypes = [vp, vp, sz, vp, C.POINTER(C.c_size_t), i64p, u32, vp]
     L.amph_base64_encode_words.argtypes = [vp, vp, sz, vp, u32, vp]
     L.amph_base64_decode_words.argtypes = [vp, vp, sz, vp, i64p, u32, vp]
+    L.amph_exchange_max_chars.restype = sz
+    L.amph_exchange_max_chars.argtypes = [sz]
+    L.amph_exchange_encode.argtypes = [vp, vp, vp, sz, vp, sz, vp, u32, vp]
+    L.amph_exchange_decode.argtypes = [vp, vp, sz, sz, vp, vp, i64p, u32, vp]
     L.amph_synth_odos.argtypes = [vp, u64, i32, sz, C.POINTER(vp), vp, C.c_int64, i32, vp]
     L.amph_synth_words.argtypes = [vp, u64, sz, vp, vp]
     return L
@@ -91,7 +95,8 @@ EXPORTED = ["amph_ctx_create", "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_
             "amph_odo_pre", "amph_open_diffs", "amph_odo_post", "amph_synth_odos",
             "amph_synth_words", "amph_host_register", "amph_host_unregister",
             "amph_time_next_launch", "amph_base64_encode", "amph_base64_decode",
-            "amph_base64_encode_words", "amph_base64_decode_words"]
+            "amph_base64_encode_words", "amph_base64_decode_words", "amph_exchange_max_chars",
+            "amph_exchange_encode", "amph_exchange_decode"]
 
 
 class _AmphOdo(C.Structure):
@@ -362,6 +367,48 @@ class Context:
             raise ValueError(lib.amph_last_error().decode())
         self._check(st)
         return out if not _is_dev(r) else (out, bad)
+
+    # -- Beaver open exchange (MultiplicationExchangeObject.interimValues) ------
+    def exchange_encode(self, mag, neg):
+        """Signed diffs (amph_odo_pre layout: mag (P, 2, 16), neg (P, 2)) -> the
+        FactorPair JSON array text.  Host arrays -> bytes; device tensors ->
+        (uint8 tensor with capacity amph_exchange_max_chars(P), length tensor)."""
+        m = mag if _is_dev(mag) else np.ascontiguousarray(mag, np.uint8)
+        g = neg if _is_dev(neg) else np.ascontiguousarray(neg, np.uint8)
+        flags, stream = self._mode(m, g)
+        P = m.shape[0]
+        cap = lib.amph_exchange_max_chars(P)
+        out = self._empty(m, (cap,))
+        if _is_dev(m):
+            import torch
+            n = torch.empty(1, dtype=torch.int64, device=m.device)
+            self._check(lib.amph_exchange_encode(self._h, _ptr(m), _ptr(g), P, _ptr(out), cap,
+                                                 C.c_void_p(n.data_ptr()), flags, stream))
+            return out, n
+        n = C.c_uint64(0)
+        self._check(lib.amph_exchange_encode(self._h, _ptr(m), _ptr(g), P, _ptr(out), cap,
+                                             C.addressof(n), flags, stream))
+        return out[: n.value].tobytes()
+
+    def exchange_decode(self, text, npairs: int):
+        """FactorPair JSON array text -> (mag (P, 2, 16), neg (P, 2)); raises
+        ValueError on a malformed token or a count other than npairs.  Device
+        uint8 tensor in -> (mag, neg, bad) device tensors, bad = AMPH_NO_FAILURE
+        when clean."""
+        if isinstance(text, str):
+            text = text.encode("utf-8")
+        a = text if _is_dev(text) else np.frombuffer(bytes(text), np.uint8)
+        n = a.numel() if _is_dev(a) else a.size
+        flags, stream = self._mode(a)
+        mag = self._empty(a, (npairs, 2, 16))
+        neg = self._empty(a, (npairs, 2))
+        bad, badp = self._ff(a)
+        st = lib.amph_exchange_decode(self._h, _ptr(a), n, npairs, _ptr(mag), _ptr(neg), badp, flags,
+                                      stream)
+        if st in (AMPH_E_PARAM, AMPH_E_LEN) and not _is_dev(a):
+            raise ValueError(lib.amph_last_error().decode())
+        self._check(st)
+        return (mag, neg) if not _is_dev(a) else (mag, neg, bad)
 
     # -- synthetic device inputs (bench / tests) --------------------------------
     def synth_odos(self, seed: int, n: int, words: int, fault_index: int = -1,

@@ -899,6 +899,122 @@ int amph_base64_decode_words(amph_ctx* c, const char* in24, size_t words, uint8_
   return st;
 }
 
+// ---- Beaver open exchange codec ------------------------------------------------
+size_t amph_exchange_max_chars(size_t npairs) { return amph::xenc_max_bytes(npairs); }
+
+namespace {
+// Host-pointer calls of the exchange codec: one shot on the context's first
+// stream (the whole text is scanned at once, so there is no batching).
+struct AsyncBuf {
+  void* p = nullptr;
+  hipStream_t s = nullptr;
+  hipError_t alloc(size_t bytes, hipStream_t st) {
+    s = st;
+    return hipMallocAsync(&p, bytes ? bytes : 16, st);
+  }
+  ~AsyncBuf() {
+    if (p) (void)hipFreeAsync(p, s);
+  }
+};
+
+int host_stream0(amph_ctx* c, hipStream_t* s) {
+  if (!c->streams[0]) HIP_TRY(hipStreamCreateWithFlags(&c->streams[0], hipStreamNonBlocking));
+  *s = c->streams[0];
+  return AMPH_OK;
+}
+}  // namespace
+
+int amph_exchange_encode(amph_ctx* c, const uint8_t* mag16, const uint8_t* neg, size_t npairs,
+                         char* out, size_t out_cap, uint64_t* out_len, uint32_t flags,
+                         void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (!out || !out_len || (npairs && (!mag16 || !neg))) return fail(AMPH_E_PARAM, "null buffer");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t maxb = amph::xenc_max_bytes(npairs);
+  if (flags & AMPH_F_DEVICE) {
+    if (out_cap < maxb) return fail(AMPH_E_LEN, "output capacity below amph_exchange_max_chars(npairs)");
+    hipStream_t s = (hipStream_t)stream;
+    AsyncBuf scratch;
+    HIP_TRY(scratch.alloc(amph::xenc_scratch_bytes(npairs), s));
+    hipError_t e = amph::launch_exchange_encode((const uint4*)mag16, neg, npairs, out,
+                                                (unsigned long long*)out_len, scratch.p, cfg(c, s, npairs));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_xenc");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  hipStream_t s;
+  if (int st = host_stream0(c, &s)) return st;
+  AsyncBuf dmag, dneg, dout, dlen, scratch;
+  HIP_TRY(dmag.alloc(32 * npairs, s));
+  HIP_TRY(dneg.alloc(2 * npairs, s));
+  HIP_TRY(dout.alloc(maxb, s));
+  HIP_TRY(dlen.alloc(8, s));
+  HIP_TRY(scratch.alloc(amph::xenc_scratch_bytes(npairs), s));
+  if (npairs) {
+    HIP_TRY(hipMemcpyAsync(dmag.p, mag16, 32 * npairs, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dneg.p, neg, 2 * npairs, hipMemcpyHostToDevice, s));
+  }
+  hipError_t e = amph::launch_exchange_encode((const uint4*)dmag.p, (const uint8_t*)dneg.p, npairs,
+                                              (char*)dout.p, (unsigned long long*)dlen.p, scratch.p,
+                                              cfg(c, s, npairs));
+  if (e != hipSuccess) return hip_fail(e, "k_xenc");
+  uint64_t len = 0;
+  HIP_TRY(hipMemcpyAsync(&len, dlen.p, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *out_len = len;
+  if (len > out_cap) return fail(AMPH_E_LEN, "output capacity " + std::to_string(out_cap) +
+                                                 " below the encoded length " + std::to_string(len));
+  HIP_TRY(hipMemcpyAsync(out, dout.p, len, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return AMPH_OK;
+}
+
+int amph_exchange_decode(amph_ctx* c, const char* text, size_t len, size_t npairs, uint8_t* mag16,
+                         uint8_t* neg, int64_t* bad_index, uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if ((len && !text) || (npairs && (!mag16 || !neg))) return fail(AMPH_E_PARAM, "null buffer");
+  HIP_TRY(hipSetDevice(c->device));
+  if (flags & AMPH_F_DEVICE) {
+    hipStream_t s = (hipStream_t)stream;
+    if (int st = reset_ff_dev(bad_index, flags, s)) return st;
+    AsyncBuf scratch;
+    HIP_TRY(scratch.alloc(amph::xdec_scratch_bytes(len), s));
+    hipError_t e = amph::launch_exchange_decode(text, len, npairs, (uint4*)mag16, neg,
+                                                (unsigned long long*)bad_index, scratch.p, cfg(c, s, len));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_xdec");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  hipStream_t s;
+  if (int st = host_stream0(c, &s)) return st;
+  AsyncBuf dtext, dmag, dneg, dbad, scratch;
+  HIP_TRY(dtext.alloc(len, s));
+  HIP_TRY(dmag.alloc(32 * npairs, s));
+  HIP_TRY(dneg.alloc(2 * npairs, s));
+  HIP_TRY(dbad.alloc(8, s));
+  HIP_TRY(scratch.alloc(amph::xdec_scratch_bytes(len), s));
+  if (len) HIP_TRY(hipMemcpyAsync(dtext.p, text, len, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(dbad.p, 0x7F, 8, s));
+  hipError_t e = amph::launch_exchange_decode((const char*)dtext.p, len, npairs, (uint4*)dmag.p,
+                                              (uint8_t*)dneg.p, (unsigned long long*)dbad.p, scratch.p,
+                                              cfg(c, s, len));
+  if (e != hipSuccess) return hip_fail(e, "k_xdec");
+  int64_t bad = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, dbad.p, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const bool ok = bad == (int64_t)AMPH_NO_FAILURE;
+  if (bad_index) *bad_index = ok ? -1 : bad;
+  if (!ok) {
+    if ((size_t)bad == len)
+      return fail(AMPH_E_LEN, "interimValues must hold exactly " + std::to_string(npairs) + " FactorPairs");
+    return fail(AMPH_E_PARAM, "Malformed FactorPair JSON at offset " + std::to_string(bad));
+  }
+  if (npairs) {
+    HIP_TRY(hipMemcpyAsync(mag16, dmag.p, 32 * npairs, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(neg, dneg.p, 2 * npairs, hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return AMPH_OK;
+}
+
 int amph_host_register(amph_ctx* c, void* ptr, size_t bytes) {
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (!ptr || !bytes) return fail(AMPH_E_PARAM, "null or empty range");

@@ -90,6 +90,17 @@ hipError_t launch_b64_words(const uint4* in, size_t words, char* out, const Laun
 hipError_t launch_b64_unwords(const char* in, size_t words, uint4* out, unsigned long long* bad,
                               const LaunchCfg& c);
 
+// Beaver open exchange codec (exchange.hip): FactorPair JSON array <-> signed
+// diffs (mag 16 B + sign byte per value, 2 values per pair).
+size_t xenc_scratch_bytes(size_t npairs);
+size_t xenc_max_bytes(size_t npairs);
+hipError_t launch_exchange_encode(const uint4* mag, const uint8_t* neg, size_t npairs, char* out,
+                                  unsigned long long* out_len, void* scratch, const LaunchCfg& c);
+size_t xdec_scratch_bytes(size_t len);
+hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, uint4* mag,
+                                  uint8_t* neg, unsigned long long* bad, void* scratch,
+                                  const LaunchCfg& c);
+
 // Synthetic honest n-party ODOs (bench/test input generator, device-side).
 struct OutSet {
   uint4* f[5][kMaxParties];

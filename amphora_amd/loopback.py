@@ -51,16 +51,23 @@ class ExchangeHub:
         self._box: Dict[uuid.UUID, Dict[int, List[FactorPair]]] = {}
         self._cv = threading.Condition()
 
-    def exchange(self, xo: MultiplicationExchangeObject) -> List[List[FactorPair]]:
+    def exchange(self, xo):
+        """xo: a MultiplicationExchangeObject (-> partners' FactorPair lists)
+        or its JSON body (-> partners' JSON bodies, as POSTed to /inter-vcp/open)."""
+        if isinstance(xo, MultiplicationExchangeObject):
+            op, pid, item = xo.operation_id, xo.player_id, list(xo.interim_values)
+        else:
+            from .wire import exchange_header
+            item = bytes(xo)
+            op, pid = exchange_header(item)
         with self._cv:
-            self._box.setdefault(xo.operation_id, {})[xo.player_id] = list(xo.interim_values)
+            self._box.setdefault(op, {})[pid] = item
             self._cv.notify_all()
-            ok = self._cv.wait_for(lambda: len(self._box[xo.operation_id]) == self.n,
-                                   timeout=self.timeout_s)
+            ok = self._cv.wait_for(lambda: len(self._box[op]) == self.n, timeout=self.timeout_s)
             if not ok:
-                raise TimeoutError("partner diffs for operation %s not received" % xo.operation_id)
-            box = self._box[xo.operation_id]
-            return [box[p] for p in sorted(box) if p != xo.player_id]
+                raise TimeoutError("partner diffs for operation %s not received" % op)
+            box = self._box[op]
+            return [box[p] for p in sorted(box) if p != pid]
 
 
 class AmphoraParty:
@@ -69,12 +76,13 @@ class AmphoraParty:
 
     def __init__(self, player_id: int, prime: int, r: int, r_inv: int, mac_key: int,
                  tuple_source: Callable[[int, uuid.UUID, str, int], bytes], hub: ExchangeHub,
-                 device: int = 0):
+                 device: int = 0, exchange_format: str = "json"):
         self.player_id = player_id
         self.ctx = _lib.Context(prime, r, r_inv, device)
         self.mac_key = mac_key
         self._castor = lambda rid, ttype, count: tuple_source(player_id, rid, ttype, count)
-        self.odo_service = OutputDeliveryService(self.ctx, player_id, self._castor, hub.exchange)
+        self.odo_service = OutputDeliveryService(self.ctx, player_id, self._castor, hub.exchange,
+                                                 exchange_format)
         self.share_util = ServiceSecretShareUtil(self.ctx)
         self.input_mask_store: Dict[uuid.UUID, object] = {}
         self.secrets: Dict[uuid.UUID, SecretShare] = {}

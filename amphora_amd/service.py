@@ -92,15 +92,22 @@ class OutputDeliveryService:
     tuple_source(request_id, tuple_type, count) -> bytes   (Castor download)
     exchange(MultiplicationExchangeObject) -> list of the partners' FactorPair
         lists in player order (open + Redis gather, recombineDiffs :231-272)
+
+    exchange_format="json": the exchange carries the MultiplicationExchangeObject
+    as its /inter-vcp/open JSON body (bytes in, partners' bodies out), coded on
+    the GPU (amph_exchange_*) -- no per-value Python objects.
     """
 
     def __init__(self, ctx: _lib.Context, player_id: int,
                  tuple_source: Callable[[uuid.UUID, str, int], bytes],
-                 exchange: Callable[[MultiplicationExchangeObject], List[List[FactorPair]]]):
+                 exchange: Callable, exchange_format: str = "objects"):
+        if exchange_format not in ("objects", "json"):
+            raise ValueError("exchange_format must be 'objects' or 'json'")
         self._ctx = ctx
         self.player_id = player_id
         self._tuples = tuple_source
         self._exchange = exchange
+        self._json = exchange_format == "json"
         self.last_exchange_object = None
 
     def _download(self, request_id, tuple_type, count):
@@ -124,18 +131,32 @@ class OutputDeliveryService:
         op_id = name_uuid_from_bytes(("%s_%d" % (request_id, 2 * W)).encode())  # :140-141
         triples = self._download(op_id, MULTIPLICATION_TRIPLE_GFP, 2 * W)
         y, r, v, mag, neg = self._ctx.odo_pre(share_words, stride, masks, triples)
-        own = decode_diffs(mag, neg)
-        xo = MultiplicationExchangeObject(op_id, self.player_id, own)
-        self.last_exchange_object = xo
-        try:
-            partners = self._exchange(xo)
-        except Exception as e:
-            raise AmphoraServiceException("Failed to open values for operation #%s" % op_id) from e
         mags, negs = [mag], [neg]
-        for lst in partners:
-            m, n = encode_diffs(lst)
-            mags.append(m)
-            negs.append(n)
+        if self._json:
+            from . import wire
+            own = wire.exchange_to_json(self._ctx, op_id, self.player_id, mag, neg)
+            self.last_exchange_object = own
+            try:
+                partners = self._exchange(own)
+                for body in partners:
+                    p_op, _, m, n = wire.exchange_from_json(self._ctx, body, mag.shape[0])
+                    if p_op != op_id:
+                        raise ValueError("operation id %s != %s" % (p_op, op_id))
+                    mags.append(m)
+                    negs.append(n)
+            except Exception as e:
+                raise AmphoraServiceException("Failed to open values for operation #%s" % op_id) from e
+        else:
+            xo = MultiplicationExchangeObject(op_id, self.player_id, decode_diffs(mag, neg))
+            self.last_exchange_object = xo
+            try:
+                partners = self._exchange(xo)
+            except Exception as e:
+                raise AmphoraServiceException("Failed to open values for operation #%s" % op_id) from e
+            for lst in partners:
+                m, n = encode_diffs(lst)
+                mags.append(m)
+                negs.append(n)
         opened = self._ctx.open_diffs(mags, negs)
         w, u = self._ctx.odo_post(opened, triples, self.player_id == 0)
         return OutputDeliveryObject(y.tobytes(), r.tobytes(), v.tobytes(), w.tobytes(), u.tobytes())

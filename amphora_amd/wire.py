@@ -158,3 +158,48 @@ def masked_input_from_json(ctx: _lib.Context, text: str) -> MaskedInput:
     else:  # MaskedInputData.of enforces the 16-byte length with the reference message
         data = [MaskedInputData.of(ctx.base64_decode(v)) for v in values]
     return MaskedInput(uuid.UUID(obj["secretId"]), data, list(obj.get("tags") or []))
+
+
+# ---- MultiplicationExchangeObject (POST /inter-vcp/open) ------------------------
+# amphora-common/.../MultiplicationExchangeObject.java:20-39: {operationId,
+# playerId, interimValues: [FactorPair{a, b}]}, the BigIntegers as JSON numbers
+# (Jackson defaults, field declaration order).  The interimValues array is
+# coded on the GPU (amph_exchange_*); the two scalar fields around it here.
+def exchange_to_json(ctx: _lib.Context, operation_id: uuid.UUID, player_id: int, mag, neg) -> bytes:
+    """Own signed diffs (amph_odo_pre layout) -> compact JSON, byte-identical to
+    Jackson's default serialisation of the MultiplicationExchangeObject."""
+    arr = ctx.exchange_encode(mag, neg)
+    if not isinstance(arr, bytes):  # device tensors -> host bytes
+        out, n = arr
+        arr = out[: int(n.item())].cpu().numpy().tobytes()
+    head = '{"operationId":"%s","playerId":%d,"interimValues":' % (operation_id, int(player_id))
+    return head.encode() + arr + b"}"
+
+
+def _exchange_split(text: bytes):
+    k = text.find(b'"interimValues"')
+    lb = text.find(b"[", k) if k >= 0 else -1
+    rb = text.rfind(b"]")
+    if k < 0 or lb < 0 or rb < lb:
+        raise IllegalArgumentException("interimValues is marked non-null but is null")
+    meta = json.loads(text[:lb] + b"[]" + text[rb + 1:])
+    for f in ("operationId", "playerId"):
+        if meta.get(f) is None:
+            raise IllegalArgumentException("%s is marked non-null but is null" % f)
+    return uuid.UUID(meta["operationId"]), int(meta["playerId"]), lb, rb
+
+
+def exchange_header(text) -> Tuple[uuid.UUID, int]:
+    """(operationId, playerId) of a MultiplicationExchangeObject JSON."""
+    text = text.encode() if isinstance(text, str) else bytes(text)
+    op, pid, _, _ = _exchange_split(text)
+    return op, pid
+
+
+def exchange_from_json(ctx: _lib.Context, text, npairs: int):
+    """JSON -> (operationId, playerId, mag (P,2,16), neg (P,2)); the array is
+    parsed on the GPU (ValueError on a malformed number or pair count)."""
+    text = text.encode() if isinstance(text, str) else bytes(text)
+    op, pid, lb, rb = _exchange_split(text)
+    mag, neg = ctx.exchange_decode(text[lb:rb + 1], npairs)
+    return op, pid, mag, neg

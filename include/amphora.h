@@ -236,6 +236,37 @@ int amph_base64_encode_words(amph_ctx* ctx, const uint8_t* words16, size_t words
 int amph_base64_decode_words(amph_ctx* ctx, const char* in24, size_t words, uint8_t* out16,
                              int64_t* bad_index, uint32_t flags, void* stream);
 
+/* ---- Beaver open exchange wire format --------------------------------------
+ * MultiplicationExchangeObject.interimValues, the FactorPair list each party
+ * sends its partners (amphora-common/.../MultiplicationExchangeObject.java:
+ * 20-39, FactorPair.java:16-25; built in OutputDeliveryService.java:186-200,
+ * consumed by recombineDiffs :231-272), as the JSON array Jackson writes:
+ * [{"a":<d_0>,"b":<e_0>},{"a":<d_1>,"b":<e_1>},...] with the signed BigIntegers
+ * as plain decimal numbers.  Replaces the Jackson (de)serialisation of that
+ * list on the /inter-vcp/open exchange.
+ *
+ * Diffs use amph_odo_pre's layout: mag16 = 2 * npairs magnitudes (LE16, d_k
+ * then e_k), neg = 2 * npairs sign bytes (nonzero = negative).
+ *
+ * encode: out gets the compact array text, byte-identical to Jackson's
+ *   default output; *out_len = its length.  Device mode: out_cap must be
+ *   >= amph_exchange_max_chars(npairs) and out_len is a device word, written
+ *   asynchronously.  Host mode: AMPH_E_LEN with *out_len = the needed length
+ *   if out_cap is too small.
+ * decode: text = the array (whitespace between tokens allowed; member order
+ *   "a","b" or "b","a").  A malformed token returns AMPH_E_PARAM with
+ *   *bad_index = its byte offset; a count other than npairs pairs returns
+ *   AMPH_E_LEN (*bad_index = len).  Magnitudes must be < 2^128.  Device mode:
+ *   bad_index is a device word (AMPH_NO_FAILURE when clean, len on a count
+ *   mismatch). */
+size_t amph_exchange_max_chars(size_t npairs);
+int amph_exchange_encode(amph_ctx* ctx, const uint8_t* mag16, const uint8_t* neg, size_t npairs,
+                         char* out, size_t out_cap, uint64_t* out_len, uint32_t flags,
+                         void* stream);
+int amph_exchange_decode(amph_ctx* ctx, const char* text, size_t len, size_t npairs,
+                         uint8_t* mag16, uint8_t* neg, int64_t* bad_index, uint32_t flags,
+                         void* stream);
+
 /* ---- benchmark / test input generation (device pointers only) ---------- */
 /* Honest n-party ODOs: out_fields[k * n_parties + j] = field k (y,r,v,w,u) of
  * party j (device, words x 16 B each).  out_plain_y (optional, device) gets the

@@ -17,7 +17,7 @@ P, R, RINV = O.TEST_PRIME, O.TEST_R, O.TEST_RINV
 SPDZ = O.MpSpdzIntegrationUtils(P, R, RINV)
 
 
-def _cluster(n, seed):
+def _cluster(n, seed, exchange_format="json"):
     import torch
     assert torch.cuda.is_available()
     from amphora_amd.loopback import AmphoraParty, ExchangeHub, LoopbackAmphoraClient
@@ -25,14 +25,18 @@ def _cluster(n, seed):
     keys = [rng.randrange(P) for _ in range(n)]
     castor = FakeCastor(P, R, RINV, keys, seed)
     hub = ExchangeHub(n)
-    parties = [AmphoraParty(j, P, R, RINV, keys[j], castor, hub) for j in range(n)]
+    parties = [AmphoraParty(j, P, R, RINV, keys[j], castor, hub, exchange_format=exchange_format)
+               for j in range(n)]
     return LoopbackAmphoraClient(parties, P, R, RINV), parties, keys, castor
 
 
-@pytest.mark.parametrize("n,W", [(2, 1000), (3, 257), (2, 1)])
-def test_upload_download_roundtrip(n, W):
+@pytest.mark.parametrize("n,W,fmt", [(2, 1000, "json"), (3, 257, "json"), (2, 1, "json"),
+                                     (2, 1000, "objects"), (3, 257, "objects")])
+def test_upload_download_roundtrip(n, W, fmt):
+    """fmt: the inter-VCP open carries MultiplicationExchangeObject JSON bodies
+    (GPU-coded) or in-memory FactorPair lists."""
     import amphora_amd as A
-    client, parties, keys, castor = _cluster(n, seed=W + n)
+    client, parties, keys, castor = _cluster(n, seed=W + n, exchange_format=fmt)
     rng = random.Random(5)
     data = [rng.randrange(2 ** 63) if i % 2 else rng.randrange(P) for i in range(W)]
     sid = client.create_secret(A.Secret.of([("k", "v")], data))
@@ -49,6 +53,11 @@ def test_upload_download_roundtrip(n, W):
     odo_req = O.odo_request_id(sid)
     assert any(c[1] == odo_req for c in castor.calls)
     assert any(c[1] == O.operation_id(odo_req, 2 * W) for c in castor.calls)
+    if fmt == "json":  # the last open each party sent is a well-formed body
+        import json
+        body = json.loads(parties[0].odo_service.last_exchange_object)
+        assert list(body) == ["operationId", "playerId", "interimValues"]
+        assert len(body["interimValues"]) == 2 * W and body["playerId"] == 0
     client.close()
 
 

@@ -159,3 +159,120 @@ def test_large_odo_json_roundtrip(ctx):
     sid2, tags, odo2 = wire.vss_from_json(ctx, text)
     assert sid2 == sid and tags == [] and odo2 == odo
     assert json.loads(text)["secretShares"] == base64.b64encode(bytes(odo.secret_shares)).decode()
+
+
+# ---- MultiplicationExchangeObject (Beaver open) ---------------------------------
+def _jackson(op, pid, pairs):
+    # Jackson's default (compact, declaration order) == json.dumps compact
+    return json.dumps({"operationId": str(op), "playerId": pid,
+                       "interimValues": [{"a": a, "b": b} for a, b in pairs]},
+                      separators=(",", ":")).encode()
+
+
+def _diff_arrays(pairs):
+    mag = np.zeros((len(pairs), 2, 16), np.uint8)
+    neg = np.zeros((len(pairs), 2), np.uint8)
+    for k, ab in enumerate(pairs):
+        for j, x in enumerate(ab):
+            mag[k, j] = np.frombuffer(abs(x).to_bytes(16, "little"), np.uint8)
+            neg[k, j] = x < 0
+    return mag, neg
+
+
+def _random_pairs(n, seed):
+    rng = random.Random(seed)
+    special = [0, 1, -1, 9, -10, 10 ** 9 - 1, 10 ** 9, -(10 ** 18), 10 ** 38, -(10 ** 38) + 1,
+               2 ** 128 - 1, -(2 ** 128 - 1), P - 1, -(P - 1), 2 ** 64, -(2 ** 96)]
+    vals = special + [rng.choice([1, -1]) * rng.randrange(P >> rng.randrange(128)) for _ in range(2 * n)]
+    vals = vals[:2 * n]
+    return [(vals[2 * k], vals[2 * k + 1]) for k in range(n)]
+
+
+def test_exchange_kat2_diffs(ctx):
+    """OutputDeliveryServiceTest.java:64-175 own diffs, as the JSON body."""
+    from amphora_amd import wire
+    pairs = [(10, 25), (39, 24), (1, 148), (294, 377)]
+    op = uuid.UUID("8065e700-9f48-36ba-ae8c-f881b28a28ef")
+    mag, neg = _diff_arrays(pairs)
+    body = wire.exchange_to_json(ctx, op, 0, mag, neg)
+    assert body == (b'{"operationId":"8065e700-9f48-36ba-ae8c-f881b28a28ef","playerId":0,'
+                    b'"interimValues":[{"a":10,"b":25},{"a":39,"b":24},{"a":1,"b":148},{"a":294,"b":377}]}')
+    op2, pid, m2, n2 = wire.exchange_from_json(ctx, body, 4)
+    assert op2 == op and pid == 0 and np.array_equal(m2, mag) and np.array_equal(n2, neg)
+
+
+@pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 5000, 100_003])
+def test_exchange_encode_matches_jackson(ctx, n):
+    from amphora_amd import wire
+    pairs = _random_pairs(n, n)
+    mag, neg = _diff_arrays(pairs)
+    neg[0, 0] = 1 if pairs[0][0] == 0 else neg[0, 0]  # a "negative zero" prints as 0
+    op = uuid.uuid4()
+    body = wire.exchange_to_json(ctx, op, 3, mag, neg)
+    assert body == _jackson(op, 3, pairs)
+    _, _, m2, n2 = wire.exchange_from_json(ctx, body, n)
+    assert np.array_equal(m2, mag)
+    neg_exp = neg.copy()
+    neg_exp[(mag == 0).all(axis=2)] = 0
+    assert np.array_equal(n2, neg_exp)
+
+
+def test_exchange_device_mode(ctx):
+    import torch
+    from amphora_amd import wire
+    pairs = _random_pairs(20_000, 1)
+    mag, neg = _diff_arrays(pairs)
+    out, ln = ctx.exchange_encode(torch.from_numpy(mag).cuda(), torch.from_numpy(neg).cuda())
+    arr = out[: int(ln.item())]
+    assert arr.cpu().numpy().tobytes() == _jackson(uuid.UUID(int=0), 0, pairs)[
+        len(b'{"operationId":"00000000-0000-0000-0000-000000000000","playerId":0,"interimValues":'):-1]
+    m2, n2, bad = ctx.exchange_decode(arr, 20_000)
+    assert int(bad.item()) == NO_FAIL_WORD
+    assert np.array_equal(m2.cpu().numpy(), mag) and np.array_equal(n2.cpu().numpy(), neg)
+    # misaligned device text (a slice at an odd offset) parses the same
+    pad = torch.cat([torch.zeros(3, dtype=torch.uint8, device="cuda"), arr])[3:]
+    m3, _, bad = ctx.exchange_decode(pad, 20_000)
+    assert int(bad.item()) == NO_FAIL_WORD and np.array_equal(m3.cpu().numpy(), mag)
+
+
+NO_FAIL_WORD = 0x7F7F7F7F7F7F7F7F
+
+
+def test_exchange_decode_whitespace_and_order(ctx):
+    """Any JSON writer's layout: pretty printing, members in either order."""
+    pairs = _random_pairs(3000, 2)
+    mag, neg = _diff_arrays(pairs)
+    items = [{"b": b, "a": a} if k % 3 == 0 else {"a": a, "b": b} for k, (a, b) in enumerate(pairs)]
+    text = json.dumps(items, indent=2).encode()
+    m2, n2 = ctx.exchange_decode(text, 3000)
+    assert np.array_equal(m2, mag)
+    assert np.array_equal(n2, neg)
+    text = json.dumps(items, separators=(" , ", " : ")).encode()
+    m3, _ = ctx.exchange_decode(b"  \n" + text + b"\n", 3000)
+    assert np.array_equal(m3, mag)
+
+
+@pytest.mark.parametrize("text,where", [
+    (b'[{"a":1,"b":2},{"a":1.5,"b":2}]', 20),
+    (b'[{"a":1,"b":2},{"a":1e5,"b":2}]', 20),
+    (b'[{"a":1,"b":2},{"a":1,"a":2}]', 26),
+    (b'[{"a":1,"b":2},{"a":1,"c":2}]', 26),
+    (b'[{"a":1,"b":2},{"a":"1","b":2}]', 21),
+    (b'[{"a":1,"b":2},{"a":1,"b":2,"a":3}]', 26),
+    (b'[{"a":1,"b":2} {"a":1,"b":2}]', 20),
+    (b'[{"a":1,"b":2},{"a":340282366920938463463374607431768211456,"b":2}]', 20),
+    (b'[{"a":1,"b":2},{"a":--1,"b":2}]', 20),
+])
+def test_exchange_decode_rejects(ctx, text, where):
+    with pytest.raises(ValueError, match="offset %d$" % where):
+        ctx.exchange_decode(text, 2)
+
+
+def test_exchange_decode_count_and_brackets(ctx):
+    with pytest.raises(ValueError, match="exactly 3 FactorPairs"):
+        ctx.exchange_decode(b'[{"a":1,"b":2},{"a":3,"b":4}]', 3)
+    with pytest.raises(ValueError, match="offset"):
+        ctx.exchange_decode(b'{"a":1,"b":2},{"a":3,"b":4}]', 2)
+    m, n = ctx.exchange_decode(b"[]", 0)
+    assert m.shape == (0, 2, 16)
+    assert ctx.exchange_encode(np.zeros((0, 2, 16), np.uint8), np.zeros((0, 2), np.uint8)) == b"[]"

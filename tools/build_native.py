@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HERE = os.path.join(ROOT, "amphora_amd")
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libamphora_hip.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("kernels.hip", "codec.hip", "capi.hip")]
+SOURCES = [os.path.join(CSRC, f) for f in ("kernels.hip", "codec.hip", "exchange.hip", "capi.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("field.hpp", "kernels.hpp", "host_stream.hpp")] + [
     os.path.join(ROOT, "include", "amphora.h")]
 ARCH = os.environ.get("AMPH_OFFLOAD_ARCH", "gfx950")
