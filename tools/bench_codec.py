@@ -43,4 +43,37 @@ out = {"stream_bytes": n,
        "words": W,
        "b64_words": {"ms": t_w, "GBps": 40 * W / (t_w * 1e-3) / 1e9},
        "b64_unwords": {"ms": t_uw, "GBps": 40 * W / (t_uw * 1e-3) / 1e9}}
+
+# Beaver open exchange (MultiplicationExchangeObject.interimValues): 2W pairs
+# of signed diffs <-> FactorPair JSON text, W = one 4 Mi-word C5 batch.
+# Bytes counted: 34 B of diffs per pair + the text.
+P2 = 2 * (1 << 22)
+mag = ctx.synth_words(2, 2 * P2).view(P2, 2, 16)
+neg = torch.randint(0, 2, (P2, 2), dtype=torch.uint8, device="cuda")
+t_xe, (txt, ln) = timed(lambda: ctx.exchange_encode(mag, neg), reps=10)
+nchars = int(ln.item())
+arr = txt[:nchars]
+t_xd, res = timed(lambda: ctx.exchange_decode(arr, P2), reps=10)
+assert int(res[2].item()) == A._lib.AMPH_NO_FAILURE
+assert torch.equal(res[0], mag)
+# CPU reference point: Python's json module on a 100k-pair sample (1 thread)
+import time  # noqa: E402
+import numpy as np  # noqa: E402
+sample = 100_000
+m_h, n_h = mag[:sample].cpu().numpy(), neg[:sample].cpu().numpy()
+vals = [int.from_bytes(m_h[k, j].tobytes(), "little") * (-1 if n_h[k, j] else 1)
+        for k in range(sample) for j in range(2)]
+t0 = time.perf_counter()
+s = json.dumps([{"a": vals[2 * k], "b": vals[2 * k + 1]} for k in range(sample)], separators=(",", ":"))
+t1 = time.perf_counter()
+back = json.loads(s)
+t2 = time.perf_counter()
+out["exchange_pairs"] = P2
+out["exchange_chars"] = nchars
+out["exchange_encode"] = {"ms": t_xe, "GBps": (34 * P2 + nchars) / (t_xe * 1e-3) / 1e9,
+                          "Mpairs_per_s": P2 / (t_xe * 1e-3) / 1e6}
+out["exchange_decode"] = {"ms": t_xd, "GBps": (34 * P2 + nchars) / (t_xd * 1e-3) / 1e9,
+                          "Mpairs_per_s": P2 / (t_xd * 1e-3) / 1e6}
+out["exchange_cpu_python_json"] = {"pairs": sample, "encode_Mpairs_per_s": sample / (t1 - t0) / 1e6,
+                                   "decode_Mpairs_per_s": sample / (t2 - t1) / 1e6}
 print(json.dumps(out))
