@@ -7,7 +7,8 @@ oracle.  Bit-exact: this is integer / byte work.
 * seeded synthetic inputs at sizes the C oracle (oracle/amphora_oracle.c)
   finishes in seconds, including non-canonical words, faults, ragged sizes,
   every party count 1..5 and 16, and a prime below 2^127;
-* BASELINE sizes (C2 1 Mi x 2 parties, C3 16 Mi x 3 parties) through
+* BASELINE sizes (C2 1 Mi x 2 parties, C3 16 Mi x 3 parties, and C4 64 Mi x 2
+  / C5 256 Mi x 3 whole on one GPU) through
   size-independent properties: verify passes on honest input, the injected
   fault is found at its index, and random word samples match the oracle.
 """
@@ -299,9 +300,11 @@ def _sample_check(F, odos_dev, y_dev, idx, host_fn):
     assert np.array_equal(host_fn(y_dev[idx]), oy)
 
 
-@pytest.mark.parametrize("n,W", [(2, 1 << 20), (3, 1 << 24)])
+@pytest.mark.parametrize("n,W", [(2, 1 << 20), (3, 1 << 24), (2, 1 << 26), (3, 1 << 28)])
 def test_baseline_sizes(ctx, F, torch, n, W):
-    """C2 (1 Mi words, 2 parties) and C3 (16 Mi words, 3 parties) on device."""
+    """C2 (1 Mi words, 2 parties), C3 (16 Mi words, 3 parties), and the whole
+    of C4 (64 Mi x 2) and C5 (256 Mi x 3, 60 GiB of shares: byte offsets far
+    past 2^32) resident on ONE GPU -- the maximum sizes BASELINE names."""
     odos, buf, _ = ctx.synth_odos(seed=99, n=n, words=W, noncanon_permille=5)
     y, ff = ctx.recombine_verify(odos)
     assert ff_dev(ff) == -1
@@ -315,7 +318,8 @@ def test_baseline_sizes(ctx, F, torch, n, W):
     sec = host(secrets[idx])
     oo, _ = F.mask_input(sec, sub_o)
     assert np.array_equal(host(masked[idx]), oo)
-    del buf
+    del buf, odos, y, secrets, masked
+    torch.cuda.empty_cache()
     # faulted: the kernel finds exactly the injected index
     fault = W // 3
     odos, buf, _ = ctx.synth_odos(seed=97, n=n, words=W, fault_index=fault)
