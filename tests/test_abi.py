@@ -81,3 +81,25 @@ def test_no_gpu_fails_loudly(native):
     c = native.Context(P, R, RINV)
     with pytest.raises(native.AmphoraNativeError, match="HIP"):
         c.recombine_verify([(np.zeros((4, 16), np.uint8),) * 5])
+
+
+def test_param_validation_before_any_device_work(native):
+    """Argument checks return AMPH_E_PARAM / AMPH_E_LEN with a message before
+    the library touches a device (runs without a GPU)."""
+    L = native._lib.lib
+    c = native.Context(P, R, RINV)
+    ff = ctypes.c_int64(0)
+    assert L.amph_recombine_verify(c._h, None, 0, None, ctypes.byref(ff), 0, None) == native._lib.AMPH_E_PARAM
+    assert b"n_parties" in L.amph_last_error()
+    assert L.amph_recombine_verify(c._h, None, 17, None, ctypes.byref(ff), 0, None) == native._lib.AMPH_E_PARAM
+    n = ctypes.c_uint64(0)
+    assert L.amph_exchange_encode(c._h, None, None, 5, None, 0, ctypes.addressof(n), 0, None) == \
+        native._lib.AMPH_E_PARAM
+    assert L.amph_exchange_decode(c._h, None, 4, 0, None, None, None, 0, None) == native._lib.AMPH_E_PARAM
+    assert L.amph_base64_decode(c._h, b"abc", 3, None, None, None, 0, None) in (
+        native._lib.AMPH_E_LEN, native._lib.AMPH_E_PARAM)
+    # {"a":-<39>,"b":-<39>}, = 92 chars per pair + the brackets
+    assert L.amph_exchange_max_chars(10) == 922
+    assert L.amph_exchange_max_chars(0) == 2
+    for code in range(6):
+        assert L.amph_strerror(code)
