@@ -7,6 +7,9 @@
 //   amphora::service::SecretShareUtil      <- amphora-service/.../calculation/SecretShareUtil.java:30-107
 //   amphora::service::OutputDeliveryService<- amphora-service/.../calculation/OutputDeliveryService.java:57-286
 //   amphora::OutputDeliveryObject          <- amphora-common/.../OutputDeliveryObject.java:55-106
+//   amphora::wire (base64, FactorPair JSON) <- Jackson on VerifiableSecretShare /
+//                                             MultiplicationExchangeObject.java:20-39
+//   amphora::nameUUIDFromBytes             <- java.util.UUID.nameUUIDFromBytes (MD5, version 3)
 //
 // Java BigIntegers become `amphora::u128` canonical integers (callers reduce
 // arbitrary-size values mod p before constructing them; `fromDecimal` does
@@ -15,6 +18,8 @@
 #ifndef AMPHORA_HPP_
 #define AMPHORA_HPP_
 
+#include <array>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <functional>
@@ -307,6 +312,200 @@ class SecretShareUtil {
 
  private:
   const Context& ctx_;
+};
+
+}  // namespace service
+
+// java.util.UUID.nameUUIDFromBytes: MD5 (RFC 1321) with the version-3 and
+// IETF-variant bits set, rendered 8-4-4-4-12 in lower-case hex.
+inline std::array<uint8_t, 16> md5(const uint8_t* msg, size_t len) {
+  uint32_t K[64];
+  for (int i = 0; i < 64; ++i) K[i] = (uint32_t)(std::fabs(std::sin((double)(i + 1))) * 4294967296.0);
+  static const int S[16] = {7, 12, 17, 22, 5, 9, 14, 20, 4, 11, 16, 23, 6, 10, 15, 21};
+  uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  Bytes m(msg, msg + len);
+  m.push_back(0x80);
+  while (m.size() % 64 != 56) m.push_back(0);
+  const uint64_t bits = (uint64_t)len * 8;
+  for (int i = 0; i < 8; ++i) m.push_back((uint8_t)(bits >> (8 * i)));
+  for (size_t off = 0; off < m.size(); off += 64) {
+    uint32_t w[16];
+    for (int i = 0; i < 16; ++i)
+      w[i] = (uint32_t)m[off + 4 * i] | ((uint32_t)m[off + 4 * i + 1] << 8) |
+             ((uint32_t)m[off + 4 * i + 2] << 16) | ((uint32_t)m[off + 4 * i + 3] << 24);
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+    for (int i = 0; i < 64; ++i) {
+      uint32_t f;
+      int g;
+      if (i < 16) { f = (b & c) | (~b & d); g = i; }
+      else if (i < 32) { f = (d & b) | (~d & c); g = (5 * i + 1) % 16; }
+      else if (i < 48) { f = b ^ c ^ d; g = (3 * i + 5) % 16; }
+      else { f = c ^ (b | ~d); g = (7 * i) % 16; }
+      const uint32_t t = d;
+      d = c;
+      c = b;
+      const uint32_t x = a + f + K[i] + w[g];
+      const int r = S[(i / 16) * 4 + i % 4];
+      b = b + ((x << r) | (x >> (32 - r)));
+      a = t;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d;
+  }
+  std::array<uint8_t, 16> out;
+  for (int i = 0; i < 16; ++i) out[i] = (uint8_t)(h[i / 4] >> (8 * (i % 4)));
+  return out;
+}
+
+inline std::string nameUUIDFromBytes(const std::string& name) {
+  auto d = md5(reinterpret_cast<const uint8_t*>(name.data()), name.size());
+  d[6] = (uint8_t)((d[6] & 0x0f) | 0x30);
+  d[8] = (uint8_t)((d[8] & 0x3f) | 0x80);
+  static const char* hex = "0123456789abcdef";
+  std::string s;
+  for (int i = 0; i < 16; ++i) {
+    if (i == 4 || i == 6 || i == 8 || i == 10) s += '-';
+    s += hex[d[i] >> 4];
+    s += hex[d[i] & 15];
+  }
+  return s;
+}
+
+namespace wire {
+
+// base64 as Jackson writes byte[] (MIME_NO_LINEFEEDS), on the GPU.
+inline std::string base64Encode(const Context& ctx, const Bytes& data) {
+  std::string out(4 * ((data.size() + 2) / 3), '\0');
+  check(amph_base64_encode(ctx.get(), data.data(), data.size(), &out[0], 0, nullptr));
+  return out;
+}
+
+inline Bytes base64Decode(const Context& ctx, const std::string& text) {
+  Bytes out(3 * text.size() / 4);
+  size_t n = 0;
+  int64_t bad = -1;
+  const int st = amph_base64_decode(ctx.get(), text.data(), text.size(), out.data(), &n, &bad, 0, nullptr);
+  if (st == AMPH_E_PARAM || st == AMPH_E_LEN) throw IllegalArgumentException(amph_last_error());
+  check(st);
+  out.resize(n);
+  return out;
+}
+
+// Signed Beaver diffs in amph_odo_pre's layout: 2 values per pair.
+struct Diffs {
+  Bytes mag;  // 32 B per pair (d, e magnitudes, LE16)
+  Bytes neg;  // 2 sign bytes per pair
+  size_t pairs() const { return neg.size() / 2; }
+};
+
+// MultiplicationExchangeObject -> its JSON body (byte-identical to Jackson's
+// default compact serialisation).
+inline std::string exchangeToJson(const Context& ctx, const std::string& operationId, int playerId,
+                                  const Diffs& d) {
+  std::string arr(amph_exchange_max_chars(d.pairs()), '\0');
+  uint64_t n = 0;
+  check(amph_exchange_encode(ctx.get(), d.mag.data(), d.neg.data(), d.pairs(), &arr[0], arr.size(), &n,
+                             0, nullptr));
+  arr.resize(n);
+  return "{\"operationId\":\"" + operationId + "\",\"playerId\":" + std::to_string(playerId) +
+         ",\"interimValues\":" + arr + "}";
+}
+
+// JSON body -> (operationId, diffs); the interimValues array is parsed on the GPU.
+inline std::pair<std::string, Diffs> exchangeFromJson(const Context& ctx, const std::string& body,
+                                                      size_t pairs) {
+  const size_t k = body.find("\"interimValues\"");
+  const size_t lb = k == std::string::npos ? k : body.find('[', k);
+  const size_t rb = body.rfind(']');
+  if (lb == std::string::npos || rb == std::string::npos || rb < lb)
+    throw IllegalArgumentException("interimValues is marked non-null but is null");
+  std::string op;
+  const size_t o = body.find("\"operationId\"");
+  if (o != std::string::npos) {
+    const size_t q0 = body.find('"', body.find(':', o) + 1);
+    const size_t q1 = q0 == std::string::npos ? q0 : body.find('"', q0 + 1);
+    if (q1 != std::string::npos) op = body.substr(q0 + 1, q1 - q0 - 1);
+  }
+  if (op.empty()) throw IllegalArgumentException("operationId is marked non-null but is null");
+  Diffs d{Bytes(32 * pairs), Bytes(2 * pairs)};
+  int64_t bad = -1;
+  const int st = amph_exchange_decode(ctx.get(), body.data() + lb, rb + 1 - lb, pairs, d.mag.data(),
+                                      d.neg.data(), &bad, 0, nullptr);
+  if (st == AMPH_E_PARAM || st == AMPH_E_LEN) throw IllegalArgumentException(amph_last_error());
+  check(st);
+  return {op, std::move(d)};
+}
+
+}  // namespace wire
+
+namespace service {
+
+// OutputDeliveryService.computeOutputDeliveryObject (:75-161) with Castor and
+// the inter-VCP open injected: tuples(requestId, tupleType, count) returns
+// the tuple stream ("INPUT_MASK_GFP": 32 B each, "MULTIPLICATION_TRIPLE_GFP":
+// 96 B each); exchange(ownJson) returns the partners' JSON bodies.
+class OutputDeliveryService {
+ public:
+  using TupleSource = std::function<Bytes(const std::string&, const std::string&, size_t)>;
+  using Exchange = std::function<std::vector<std::string>(const std::string&)>;
+
+  OutputDeliveryService(const Context& ctx, int playerId, TupleSource tuples, Exchange exchange)
+      : ctx_(ctx), playerId_(playerId), tuples_(std::move(tuples)), exchange_(std::move(exchange)) {}
+
+  // shareData: SecretShare.data (stride 32, MACs stripped) or raw words (stride 16)
+  OutputDeliveryObject computeOutputDeliveryObject(const Bytes& shareData, size_t stride,
+                                                   const std::string& requestId) {
+    const size_t W = shareData.size() / stride;
+    const Bytes masks = download(requestId, "INPUT_MASK_GFP", 2 * W, 32);
+    const std::string op = nameUUIDFromBytes(requestId + "_" + std::to_string(2 * W));  // :140-141
+    const Bytes triples = download(op, "MULTIPLICATION_TRIPLE_GFP", 2 * W, 96);
+    Bytes y(16 * W), r(16 * W), v(16 * W);
+    wire::Diffs own{Bytes(64 * W), Bytes(4 * W)};
+    check(amph_odo_pre(ctx_.get(), shareData.data(), stride, masks.data(), triples.data(), W, y.data(),
+                       r.data(), v.data(), own.mag.data(), own.neg.data(), 0, nullptr));
+    lastExchange_ = wire::exchangeToJson(ctx_, op, playerId_, own);
+    std::vector<wire::Diffs> partners;
+    try {
+      for (const std::string& body : exchange_(lastExchange_)) {
+        auto pd = wire::exchangeFromJson(ctx_, body, 2 * W);
+        if (pd.first != op) throw IllegalArgumentException("operation id mismatch");
+        partners.push_back(std::move(pd.second));
+      }
+    } catch (const std::exception&) {
+      throw AmphoraServiceException("Failed to open values for operation #" + op);
+    }
+    std::vector<const uint8_t*> mags{own.mag.data()}, negs{own.neg.data()};
+    for (auto& pd : partners) {
+      mags.push_back(pd.mag.data());
+      negs.push_back(pd.neg.data());
+    }
+    Bytes opened(64 * W), w(16 * W), u(16 * W);
+    check(amph_open_diffs(ctx_.get(), mags.data(), negs.data(), (int)mags.size(), 2 * W, opened.data(), 0,
+                          nullptr));
+    check(amph_odo_post(ctx_.get(), opened.data(), triples.data(), W, playerId_ == 0, w.data(), u.data(), 0,
+                        nullptr));
+    return OutputDeliveryObject(std::move(y), std::move(r), std::move(v), std::move(w), std::move(u));
+  }
+
+  const std::string& lastExchangeObject() const { return lastExchange_; }
+
+ private:
+  Bytes download(const std::string& id, const char* type, size_t count, size_t width) {
+    Bytes b;
+    try {
+      b = tuples_(id, type, count);
+    } catch (const std::exception&) {  // :103-107, :178-185
+      throw AmphoraServiceException("Failed to retrieve the required Tuples form Castor");
+    }
+    if (b.size() != count * width)
+      throw AmphoraServiceException("Failed to retrieve the required Tuples form Castor");
+    return b;
+  }
+
+  const Context& ctx_;
+  int playerId_;
+  TupleSource tuples_;
+  Exchange exchange_;
+  std::string lastExchange_;
 };
 
 }  // namespace service

@@ -48,6 +48,60 @@ static void cpu_tests() {
     threw = std::string(e.what()) == "The provided shares must be of the same length";
   }
   EXPECT(threw);
+  // java.util.UUID.nameUUIDFromBytes (OutputDeliveryServiceTest.java operation id)
+  auto d0 = md5(nullptr, 0);
+  EXPECT(d0[0] == 0xd4 && d0[1] == 0x1d && d0[15] == 0x7e);  // md5("") = d41d8c...f8427e
+  EXPECT(nameUUIDFromBytes("70297fd4-d412-4dbb-af05-6818fe0e687a_4") == "8065e700-9f48-36ba-ae8c-f881b28a28ef");
+}
+
+// KAT-2 (OutputDeliveryServiceTest.java:64-175) through the C++ service, the
+// open carried as MultiplicationExchangeObject JSON bodies.
+static void kat2_service(const Context& c) {
+  const std::vector<u128> secrets = {90, 142}, masks = {87, 111, 412, 313};
+  const u128 tri[4][3] = {{80, 62, 3719}, {72, 63, 32521}, {141, 264, 56212}, {19, 35, 612}};
+  auto g = [&](u128 x) { return c.toGfp({x}); };
+  auto cat = [](Bytes& a, const Bytes& b) { a.insert(a.end(), b.begin(), b.end()); };
+  Bytes share, maskTuples, triples;
+  for (u128 s : secrets) { cat(share, g(s)); cat(share, g(0)); }
+  for (u128 m : masks) { cat(maskTuples, g(m)); cat(maskTuples, g(0)); }
+  for (auto& t : tri)
+    for (int k = 0; k < 3; ++k) { cat(triples, g(t[k])); cat(triples, g(0)); }
+  const std::string req = "70297fd4-d412-4dbb-af05-6818fe0e687a", op = "8065e700-9f48-36ba-ae8c-f881b28a28ef";
+  const std::string own = "{\"operationId\":\"" + op + "\",\"playerId\":0,\"interimValues\":"
+                          "[{\"a\":10,\"b\":25},{\"a\":39,\"b\":24},{\"a\":1,\"b\":148},{\"a\":294,\"b\":377}]}";
+  const std::string partner = "{\"operationId\":\"" + op + "\",\"playerId\":1,\"interimValues\":"
+                              "[{\"a\":4,\"b\":63},{\"a\":175,\"b\":136},{\"a\":5,\"b\":106},{\"a\":2,\"b\":27}]}";
+  bool ownOk = false;
+  service::OutputDeliveryService svc(
+      c, 0,
+      [&](const std::string& id, const std::string& type, size_t count) {
+        EXPECT(count == 4);
+        if (type == "INPUT_MASK_GFP") { EXPECT(id == req); return maskTuples; }
+        EXPECT(type == "MULTIPLICATION_TRIPLE_GFP" && id == op);
+        return triples;
+      },
+      [&](const std::string& body) {
+        ownOk = body == own;
+        return std::vector<std::string>{partner};
+      });
+  OutputDeliveryObject odo = svc.computeOutputDeliveryObject(share, 32, req);
+  EXPECT(ownOk);
+  EXPECT(odo == OutputDeliveryObject(c.toGfp(secrets), c.toGfp({87, 412}), c.toGfp({111, 313}),
+                                     c.toGfp({12859, 95134}), c.toGfp({91763, 138232})));
+  bool threw = false;
+  service::OutputDeliveryService broken(
+      c, 0, [&](const std::string&, const std::string&, size_t) -> Bytes { throw std::runtime_error("x"); },
+      [&](const std::string&) { return std::vector<std::string>{}; });
+  try {
+    broken.computeOutputDeliveryObject(share, 32, req);
+  } catch (const AmphoraServiceException& e) {
+    threw = std::string(e.what()) == "Failed to retrieve the required Tuples form Castor";
+  }
+  EXPECT(threw);
+  // base64 as Jackson writes byte[] (VerifiableSecretTest.java)
+  const std::string b = wire::base64Encode(c, Bytes{'s', 'S', 'h', 'a', 'r', 'e', 's'});
+  EXPECT(b == "c1NoYXJlcw==");
+  EXPECT(wire::base64Decode(c, b) == (Bytes{'s', 'S', 'h', 'a', 'r', 'e', 's'}));
 }
 
 static void gpu_tests() {
@@ -148,7 +202,11 @@ int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "cpu";
   try {
     cpu_tests();
-    if (mode == "gpu") gpu_tests();
+    if (mode == "gpu") {
+      gpu_tests();
+      Context c(P, R, RI);
+      kat2_service(c);
+    }
   } catch (const std::exception& e) {
     std::fprintf(stderr, "exception: %s\n", e.what());
     return 2;

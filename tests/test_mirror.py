@@ -115,6 +115,30 @@ def test_kat2_compute_output_delivery_object(A, ctx, kat):
     assert odo == expected
 
 
+def test_kat2_json_exchange(A, ctx, kat):
+    """The same KAT with the open carried as MultiplicationExchangeObject JSON
+    bodies (exchange_format="json", GPU-coded)."""
+    import json
+    from amphora_amd.service import OutputDeliveryService
+    k = kat["kat2"]
+    svc0, req, _ = _kat2_service(A, ctx, kat)
+    seen = []
+
+    def exchange(body):
+        seen.append(body)
+        return [json.dumps({"operationId": k["expected_operation_id"], "playerId": 1,
+                            "interimValues": [{"a": a, "b": b} for a, b in k["partner_diffs"]]},
+                           separators=(",", ":")).encode()]
+
+    svc = OutputDeliveryService(ctx, k["player_id"], svc0._tuples, exchange, exchange_format="json")
+    share = A.SecretShare(None, b"".join(SPDZ.to_gfp(v) + SPDZ.to_gfp(0) for v in k["secret_values"]))
+    odo = svc.compute_output_delivery_object(share, req)
+    assert seen[0] == json.dumps({"operationId": k["expected_operation_id"], "playerId": 0,
+                                  "interimValues": [{"a": a, "b": b} for a, b in k["expected_own_diffs"]]},
+                                 separators=(",", ":")).encode()
+    assert odo == svc0.compute_output_delivery_object(share, req)
+
+
 def test_kat2_failure_messages(A, ctx, kat):
     k = kat["kat2"]
     share = A.SecretShare(None, b"".join(SPDZ.to_gfp(v) + SPDZ.to_gfp(0) for v in k["secret_values"]))
