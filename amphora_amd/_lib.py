@@ -51,6 +51,9 @@ def _load():
     L = C.CDLL(LIB_PATH)
     vp, sz, i32, u32, u64, i64p = C.c_void_p, C.c_size_t, C.c_int, C.c_uint32, C.c_uint64, C.POINTER(C.c_int64)
     L.amph_ctx_create.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, i32, C.POINTER(vp)]
+    L.amph_ctx_create_multi.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(i32), i32,
+                                        C.POINTER(vp)]
+    L.amph_ctx_device_count.argtypes = [vp]
     L.amph_ctx_destroy.argtypes = [vp]
     L.amph_ctx_device.argtypes = [vp]
     L.amph_ctx_set_batch_words.argtypes = [vp, sz]
@@ -88,7 +91,7 @@ def _load():
 
 lib = _load()
 
-EXPORTED = ["amph_ctx_create", "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_set_batch_words",
+EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count", "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_set_batch_words",
             "amph_strerror", "amph_last_error", "amph_version", "amph_recombine_verify",
             "amph_mask_input", "amph_recombine", "amph_verify", "amph_verify_message",
             "amph_mask_words", "amph_to_gfp", "amph_from_gfp", "amph_convert_share",
@@ -135,12 +138,24 @@ def _ptr(x):
 class Context:
     """One amph_ctx: field parameters (prime, r, rInv) bound to one GPU."""
 
-    def __init__(self, prime: int, r: int, r_inv: int, device: int = 0):
+    def __init__(self, prime: int, r: int, r_inv: int, device: int = 0, devices=None):
+        """devices: several GPU ordinals -> amph_ctx_create_multi (host-pointer
+        calls are sharded over them); device-pointer calls use devices[0]."""
+        if devices is not None and len(devices) > 0:
+            device = int(devices[0])
         self.prime, self.r, self.r_inv, self.device = prime, r, r_inv, device
         h = C.c_void_p()
-        self._check(lib.amph_ctx_create(le16(prime % (1 << 128)), le16(r % (1 << 128)),
-                                        le16(r_inv % (1 << 128)), device, C.byref(h)))
+        keys = (le16(prime % (1 << 128)), le16(r % (1 << 128)), le16(r_inv % (1 << 128)))
+        if devices is not None and len(devices) > 1:
+            arr = (C.c_int * len(devices))(*[int(d) for d in devices])
+            self._check(lib.amph_ctx_create_multi(*keys, arr, len(devices), C.byref(h)))
+        else:
+            self._check(lib.amph_ctx_create(*keys, device, C.byref(h)))
         self._h = h
+
+    @property
+    def device_count(self) -> int:
+        return lib.amph_ctx_device_count(self._h)
 
     def __del__(self):
         h = getattr(self, "_h", None)

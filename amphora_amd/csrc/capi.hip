@@ -116,6 +116,7 @@ struct amph_ctx {
   };
   hipStream_t streams[kSlots] = {};
   Slot slots[kSlots];
+  std::vector<amph_ctx*> sub;  // amph_ctx_create_multi: one context per device
   DevBuf ff;  // per-batch first-fail words (host path)
   DevBuf tail;  // small scratch for the partial last unit of codec calls
   std::unique_ptr<amph::CopyPool> pool;
@@ -198,6 +199,11 @@ int host_threads() {
   return (int)std::max(1u, std::min(8u, hw ? hw / 2 : 1u));
 }
 
+template <class Launch>
+int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
+                const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
+                Launch& launch);
+
 // Streams `words` through the device in batches of ctx->batch_words:
 //   stage inputs (CPU threads: pageable -> page-locked slot), HtoD, kernel,
 //   DtoH (-> page-locked slot), and copy outputs back once the slot's event
@@ -210,6 +216,7 @@ template <class Launch>
 int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
                 const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
                 Launch&& launch) {
+  if (!c->sub.empty()) return run_sharded(c, words, ins, outs, with_ff, first_fail, launch);
   if (first_fail) *first_fail = -1;
   if (words == 0) return AMPH_OK;
   constexpr int S = amph_ctx::kSlots;
@@ -326,6 +333,52 @@ int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
   return AMPH_OK;
 }
 
+// Multi-device context: contiguous shards of ceil(words / ndev), one thread
+// per device running that device's own batched pipeline; the first failing
+// shard (in word order) gives the global first-fail index.
+template <class Launch>
+int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
+                const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
+                Launch& launch) {
+  if (first_fail) *first_fail = -1;
+  g_ev_start = g_ev_stop = nullptr;  // per-launch timing is single-device only
+  if (words == 0) return AMPH_OK;
+  const size_t nd = g->sub.size(), per = (words + nd - 1) / nd;
+  struct Res {
+    int st = AMPH_OK;
+    int64_t ff = -1;
+    std::string err;
+  };
+  std::vector<Res> res(nd);
+  std::vector<std::thread> th;
+  for (size_t d = 0; d < nd && d * per < words; ++d) {
+    const size_t start = d * per, cnt = std::min(per, words - start);
+    std::vector<HostIn> in2(ins);
+    for (auto& x : in2) x.host += start * x.bytes_per_word;
+    std::vector<HostOut> out2(outs);
+    for (auto& x : out2) x.host += start * x.bytes_per_word;
+    th.emplace_back([&, d, cnt, in2 = std::move(in2), out2 = std::move(out2)]() {
+      amph_ctx* s = g->sub[d];
+      try {
+        std::lock_guard<std::mutex> lk(s->mu);
+        res[d].st = run_batched(s, cnt, in2, out2, with_ff, &res[d].ff, launch);
+      } catch (const std::exception& e) {
+        res[d].st = fail(AMPH_E_NOMEM, e.what());
+      }
+      if (res[d].st != AMPH_OK) res[d].err = g_last_error;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (size_t d = 0; d < th.size(); ++d)
+    if (res[d].st != AMPH_OK && res[d].st != AMPH_E_VERIFY) return fail(res[d].st, res[d].err);
+  for (size_t d = 0; d < th.size(); ++d)
+    if (res[d].st == AMPH_E_VERIFY) {
+      if (first_fail) *first_fail = (int64_t)(d * per) + res[d].ff;
+      return AMPH_E_VERIFY;
+    }
+  return AMPH_OK;
+}
+
 int check_ctx(amph_ctx* c) { return c ? AMPH_OK : fail(AMPH_E_PARAM, "null context"); }
 
 int odo_words(const amph_odo* odos, int n, size_t* words) {
@@ -409,8 +462,34 @@ int amph_ctx_create(const uint8_t p_le[16], const uint8_t r_le[16], const uint8_
   return AMPH_OK;
 }
 
+int amph_ctx_create_multi(const uint8_t p_le[16], const uint8_t r_le[16],
+                          const uint8_t rinv_le[16], const int* devices, int ndev,
+                          amph_ctx** out) {
+  if (!out || !devices || ndev < 1) return fail(AMPH_E_PARAM, "devices must name at least one device");
+  if (ndev == 1) return amph_ctx_create(p_le, r_le, rinv_le, devices[0], out);
+  *out = nullptr;
+  amph_ctx* g = nullptr;
+  if (int st = amph_ctx_create(p_le, r_le, rinv_le, devices[0], &g)) return st;
+  for (int d = 0; d < ndev; ++d) {
+    amph_ctx* s = nullptr;
+    if (int st = amph_ctx_create(p_le, r_le, rinv_le, devices[d], &s)) {
+      amph_ctx_destroy(g);
+      return st;
+    }
+    g->sub.push_back(s);
+  }
+  *out = g;
+  return AMPH_OK;
+}
+
+int amph_ctx_device_count(const amph_ctx* c) {
+  return c ? (c->sub.empty() ? 1 : (int)c->sub.size()) : 0;
+}
+
 void amph_ctx_destroy(amph_ctx* c) {
   if (!c) return;
+  for (amph_ctx* s : c->sub) amph_ctx_destroy(s);
+  c->sub.clear();
   if (c->streams[0] || c->slots[0].dev.p || c->ff.p) {
     (void)hipSetDevice(c->device);
     for (int s = 0; s < amph_ctx::kSlots; ++s) {
@@ -433,6 +512,7 @@ int amph_ctx_set_batch_words(amph_ctx* c, size_t words) {
   if (check_ctx(c)) return AMPH_E_PARAM;
   std::lock_guard<std::mutex> g(c->mu);
   if (words) c->batch_words = words;
+  for (amph_ctx* s : c->sub) amph_ctx_set_batch_words(s, words);
   return AMPH_OK;
 }
 
@@ -1019,7 +1099,7 @@ int amph_host_register(amph_ctx* c, void* ptr, size_t bytes) {
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (!ptr || !bytes) return fail(AMPH_E_PARAM, "null or empty range");
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterPortable));
   return AMPH_OK;
 }
 

@@ -56,6 +56,9 @@ def parse():
                     help="host: inputs/outputs in host memory (PCIe-inclusive rate, C5)")
     ap.add_argument("--pin", action="store_true", help="host mode: page-lock the inputs first")
     ap.add_argument("--batch-words", type=int, default=4 << 20)
+    ap.add_argument("--host-devices", default="",
+                    help="host mode: comma list of device ordinals for one amph_ctx_create_multi "
+                         "context (each GPU streams its own shard over its own PCIe link)")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) on the GPU node; gloo to "
                     "rehearse several ranks on one GPU")
     ap.add_argument("--same-device", action="store_true",
@@ -153,14 +156,17 @@ def host_mode(a, A, torch, ctx):
     pipeline) and writes the masked words and canonical secrets back to host
     memory.  Not the headline metric; recorded in DESIGN.md."""
     W, n = a.words, a.parties
+    gen = ctx
+    if a.host_devices:  # one context over several devices: per-GPU shards from host memory
+        ctx = A.Context(ctx.prime, ctx.r, ctx.r_inv, devices=[int(d) for d in a.host_devices.split(",")])
     ctx.set_batch_words(a.batch_words)
-    _, mb, _ = ctx.synth_odos(seed=11, n=n, words=W)
+    _, mb, _ = gen.synth_odos(seed=11, n=n, words=W)
     mask_h = mb.cpu().numpy()
     del mb
-    _, sb, _ = ctx.synth_odos(seed=12, n=n, words=W)
+    _, sb, _ = gen.synth_odos(seed=12, n=n, words=W)
     share_h = sb.cpu().numpy()
     del sb
-    sec_h = ctx.synth_words(seed=13, count=W).cpu().numpy()
+    sec_h = gen.synth_words(seed=13, count=W).cpu().numpy()
     torch.cuda.empty_cache()
     mask_odos = [tuple(mask_h[k, j] for k in range(5)) for j in range(n)]
     share_odos = [tuple(share_h[k, j] for k in range(5)) for j in range(n)]
@@ -179,7 +185,7 @@ def host_mode(a, A, torch, ctx):
     el = time.perf_counter() - t0
     hbytes = (kbytes("k_mask", n) + kbytes("k_rv", n)) * W
     line = {"metric": "secret words/s host-memory share+recombine (PCIe-inclusive)",
-            "value": W * a.steps / el, "unit": "words/s", "n_gpus": 1, "steps": a.steps,
+            "value": W * a.steps / el, "unit": "words/s", "n_gpus": ctx.device_count, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": el * 1e3 / a.steps, "higher_is_better": True,
             "verified": ok, "pinned_inputs": a.pin, "batch_words": a.batch_words,
             "host_bytes_per_step": hbytes, "host_GBps": hbytes * a.steps / el / 1e9,

@@ -106,16 +106,31 @@ typedef struct amph_odo {
  * and r * rInv == 1 (mod p).  `device` = HIP device ordinal. */
 int amph_ctx_create(const uint8_t p_le[16], const uint8_t r_le[16], const uint8_t rinv_le[16],
                     int device, amph_ctx** out);
+/* Several GPUs behind one context (SURVEY.md 8b's amph_ctx_create(...,
+ * const int* devices, int ndev, ...)): host-pointer calls split their word
+ * range into ndev contiguous shards, stream each through its own device
+ * concurrently (every shard with its own 3-slot pipeline and staging
+ * threads) and report the smallest failing word index over all shards --
+ * SURVEY.md 8e's "direct per-GPU HtoD from pinned memory" for host-origin
+ * data (C5).  Device-pointer calls (AMPH_F_DEVICE) and the exchange codec
+ * run on devices[0].  A device may appear more than once.  ndev == 1 is
+ * amph_ctx_create. */
+int amph_ctx_create_multi(const uint8_t p_le[16], const uint8_t r_le[16],
+                          const uint8_t rinv_le[16], const int* devices, int ndev,
+                          amph_ctx** out);
 void amph_ctx_destroy(amph_ctx* ctx);
 int amph_ctx_device(const amph_ctx* ctx);
+/* Number of devices behind the context (1 unless amph_ctx_create_multi). */
+int amph_ctx_device_count(const amph_ctx* ctx);
 /* Host-path batch size in words (default 4 Mi); 0 keeps the current value.
  * Host-pointer calls stream their arrays through the GPU batch by batch:
  * pageable caller memory is staged through page-locked buffers by CPU
  * threads (AMPH_HOST_THREADS, default min(8, cores/2)) with HtoD, kernel and
  * DtoH of consecutive batches overlapped on 3 HIP streams. */
 int amph_ctx_set_batch_words(amph_ctx* ctx, size_t words);
-/* Page-lock a caller buffer (hipHostRegister) so host-pointer calls DMA it
- * directly without the staging copy (e.g. a long-lived direct ByteBuffer). */
+/* Page-lock a caller buffer (hipHostRegister, portable to every device) so
+ * host-pointer calls DMA it directly without the staging copy (e.g. a
+ * long-lived direct ByteBuffer). */
 int amph_host_register(amph_ctx* ctx, void* ptr, size_t bytes);
 int amph_host_unregister(amph_ctx* ctx, void* ptr);
 

@@ -103,3 +103,18 @@ def test_param_validation_before_any_device_work(native):
     assert L.amph_exchange_max_chars(0) == 2
     for code in range(6):
         assert L.amph_strerror(code)
+
+
+def test_multi_device_context_validation(native):
+    """amph_ctx_create_multi: argument checks and device count (no GPU work)."""
+    L = native._lib.lib
+    h = ctypes.c_void_p()
+    keys = [native._lib.le16(x) for x in (P, R, RINV)]
+    assert L.amph_ctx_create_multi(*keys, None, 2, ctypes.byref(h)) == native._lib.AMPH_E_PARAM
+    devs = (ctypes.c_int * 3)(0, 0, 0)
+    assert L.amph_ctx_create_multi(*keys, devs, 0, ctypes.byref(h)) == native._lib.AMPH_E_PARAM
+    c = native.Context(P, R, RINV, devices=[0, 0, 0])
+    assert c.device_count == 3 and c.device == 0
+    assert native.Context(P, R, RINV, devices=[0]).device_count == 1
+    with pytest.raises(native.AmphoraNativeError, match="inverse"):
+        native.Context(P, R, RINV + 1, devices=[0, 0])

@@ -208,6 +208,46 @@ def test_concurrent_callers(ctx, F):
         assert ff == off and np.array_equal(y, oy)
 
 
+def test_multi_device_context(ctx, F):
+    """amph_ctx_create_multi with the one GPU named three times: host-pointer
+    calls run as three concurrent shards (each its own batched pipeline) and
+    must equal the single-device results, with global first-fail indices."""
+    import amphora_amd as A
+    g = A.Context(P, R, RINV, devices=[0, 0, 0])
+    g.set_batch_words(8192)  # several batches per shard
+    W = 100_003  # shards of 33 335 words
+    for fault in (-1, 70_000, 33_334, 33_335):
+        odos, _ = F.synth_odos(seed=600, n=3, W=W, fault_index=fault, noncanon_permille=10)
+        y, ff = g.recombine_verify(odos)
+        oy, off = F.recombine_verify(odos)
+        assert ff == off == fault and np.array_equal(y, oy), fault
+    # two faults in different shards: the smaller index wins
+    odos, _ = F.synth_odos(seed=601, n=2, W=W, fault_index=90_000)
+    odos[1][4][40_000, 0] ^= 1
+    assert g.recombine_verify(odos)[1] == 40_000
+    # masking with fewer secrets than masks: the verify-only tail is sharded too
+    odos, _ = F.synth_odos(seed=602, n=2, W=W, fault_index=95_000)
+    secrets = F.synth_words(seed=603, count=60_000, mont=False)
+    out, ff = g.mask_input(odos, secrets)
+    assert ff == 95_000
+    odos, _ = F.synth_odos(seed=602, n=2, W=W)
+    out, ff = g.mask_input(odos, secrets)
+    oo, _ = F.mask_input(secrets, [tuple(f[:60_000] for f in o) for o in odos])
+    assert ff == -1 and np.array_equal(out, oo)
+    # other word-parallel calls agree with the single-device context
+    words = F.synth_words(seed=604, count=W, mont=True)
+    assert np.array_equal(g.from_gfp(words), ctx.from_gfp(words))
+    assert np.array_equal(g.to_gfp(words), ctx.to_gfp(words))
+    tuples = F.synth_words(seed=605, count=2 * W, mont=True).reshape(W, 32)
+    assert np.array_equal(g.convert_share(words, tuples, 12345, False),
+                          ctx.convert_share(words, tuples, 12345, False))
+    assert np.array_equal(g.base64_encode_words(words), ctx.base64_encode_words(words))
+    # fewer words than devices
+    odos, _ = F.synth_odos(seed=606, n=2, W=2)
+    y, ff = g.recombine_verify(odos)
+    assert ff == -1 and np.array_equal(y, F.recombine_verify(odos)[0])
+
+
 def test_empty_and_single(ctx):
     z = np.zeros((0, 16), np.uint8)
     y, ff = ctx.recombine_verify([(z,) * 5, (z,) * 5])
