@@ -10,7 +10,7 @@ native library and raises if it is missing: there is no CPU fallback.
 """
 from . import _lib  # noqa: F401  (loads libamphora_hip.so or raises)
 from ._lib import Context, AmphoraNativeError  # noqa: F401
-from .entities import (AmphoraServiceException, FactorPair, IllegalArgumentException,  # noqa: F401
+from .entities import (AmphoraClientException, AmphoraServiceException, FactorPair, IllegalArgumentException,  # noqa: F401
                        IntegrityVerificationException, MaskedInput, MaskedInputData,
                        MultiplicationExchangeObject, OutputDeliveryObject, Secret, SecretShare)
 

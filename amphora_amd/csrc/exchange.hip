@@ -263,14 +263,28 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_count(const uint8_t* t, size
   if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-__device__ __forceinline__ size_t skip_ws_back(const uint8_t* t, size_t q) {  // q: index+1
+// The workgroup's text window (its 8 KiB plus 256 B either side) staged in
+// LDS; bytes outside it (long whitespace runs) come from global memory.
+struct Window {
+  const uint8_t* t;
+  const uint8_t* lds;
+  size_t w0, w1;
+  __device__ __forceinline__ uint32_t operator[](size_t x) const {
+    return x - w0 < w1 - w0 ? lds[x - w0] : t[x];
+  }
+};
+constexpr int kWinPad = 256;
+
+template <class T>
+__device__ __forceinline__ size_t skip_ws_back(const T& t, size_t q) {  // q: index+1
   while (q > 0 && is_ws(t[q - 1])) --q;
   return q;
 }
 
 // Backward from just before a number start x: ws ':' ws '"' key '"' ws.
 // Returns the key char (or 0), *q = index+1 of the byte before the key.
-__device__ __forceinline__ uint32_t key_before(const uint8_t* t, size_t x, size_t* q) {
+template <class T>
+__device__ __forceinline__ uint32_t key_before(const T& t, size_t x, size_t* q) {
   size_t p = skip_ws_back(t, x);
   if (p == 0 || t[p - 1] != ':') return 0;
   p = skip_ws_back(t, p - 1);
@@ -281,14 +295,20 @@ __device__ __forceinline__ uint32_t key_before(const uint8_t* t, size_t x, size_
   return k;
 }
 
-__global__ __launch_bounds__(kDecBlock) void k_xdec_parse(const uint8_t* t, size_t len,
+__global__ __launch_bounds__(kDecBlock) void k_xdec_parse(const uint8_t* text, size_t len,
                                                       const uint64_t* bscan, size_t nvals,
                                                       uint4* mag, uint8_t* neg,
                                                       unsigned long long* bad) {
-  const size_t base = ((size_t)blockIdx.x * kDecBlock + threadIdx.x) * kDecBytes;
-  uint32_t m = base < len ? start_mask(t, len, base) : 0;
+  __shared__ uint8_t win[kDecBlock * kDecBytes + 2 * kWinPad];
+  const size_t b0 = (size_t)blockIdx.x * kDecBlock * kDecBytes;
+  const size_t w0 = b0 > (size_t)kWinPad ? b0 - kWinPad : 0;
+  const size_t w1 = min(len, b0 + (size_t)kDecBlock * kDecBytes + kWinPad);
+  for (size_t i = threadIdx.x; i < w1 - w0; i += kDecBlock) win[i] = text[w0 + i];
+  const Window t{text, win, w0, w1};
+  const size_t base = b0 + (size_t)threadIdx.x * kDecBytes;
+  uint32_t m = base < len ? start_mask(text, len, base) : 0;
   uint64_t total;
-  uint64_t g = bscan[blockIdx.x] + block_excl_scan(__popc(m), &total);
+  uint64_t g = bscan[blockIdx.x] + block_excl_scan(__popc(m), &total);  // (its barriers also publish win)
   for (; m; m &= m - 1, ++g) {
     const size_t x = base + __ffs(m) - 1;
     size_t q = 0;

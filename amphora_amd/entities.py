@@ -32,6 +32,11 @@ class AmphoraServiceException(RuntimeError):
     """AmphoraServiceException.java:16-37."""
 
 
+class AmphoraClientException(Exception):
+    """AmphoraClientException (amphora-java-client): a failed request to at
+    least one party (DefaultAmphoraClient.java:613-638, 693-728)."""
+
+
 class OutputDeliveryObject:
     FIELDS = ("secret_shares", "r_shares", "v_shares", "w_shares", "u_shares")
 

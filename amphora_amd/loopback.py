@@ -32,12 +32,13 @@ from typing import Callable, Dict, List, Sequence
 
 from . import _lib
 from .client import SecretShareUtil, create_masked_input, verify_output_delivery_objects
-from .entities import (AmphoraServiceException, FactorPair, MaskedInput,
+from .entities import (AmphoraClientException, AmphoraServiceException, FactorPair, MaskedInput,
                        MultiplicationExchangeObject, OutputDeliveryObject, Secret, SecretShare)
 from .service import INPUT_MASK_GFP, OutputDeliveryService
 from .service import SecretShareUtil as ServiceSecretShareUtil
 
 NO_INPUT_MASKS_FOUND_FOR_REQUEST_ID_EXCEPTION_MSG = "No input masks found for request ID %s"
+REQUEST_FOR_ENDPOINT_FAILED_EXCEPTION_MSG = 'Request for endpoint "%s" failed: %s'  # DefaultAmphoraClient.java:81-82
 
 
 class ExchangeHub:
@@ -120,19 +121,48 @@ class LoopbackAmphoraClient:
         self.util = SecretShareUtil.of(prime, r, r_inv, device)
         self._pool = ThreadPoolExecutor(max_workers=len(self.parties))
 
+    @staticmethod
+    def uri(party) -> str:
+        return "loopback://amphora-%d" % party.player_id
+
     def _fan_out(self, fn):
+        """One Try per party, like AmphoraCommunicationClient's results map."""
         futs = [self._pool.submit(fn, p) for p in self.parties]
-        return [f.result() for f in futs]
+        out = []
+        for p, f in zip(self.parties, futs):
+            try:
+                out.append((p, f.result(), None))
+            except Exception as e:  # noqa: BLE001 -- a failed request, reported below
+                out.append((p, None, e))
+        return out
+
+    @staticmethod
+    def _unwrap(tries):
+        """DefaultAmphoraClient.unwrap :693-711."""
+        failures = [e for _, _, e in tries if e is not None]
+        if failures:
+            raise AmphoraClientException("Error(s) occurred while processing responses:\n\t%s"
+                                         % "\n\t".join(str(e) for e in failures))
+        return [v for _, v, _ in tries]
+
+    def _check_success(self, tries):
+        """DefaultAmphoraClient.checkSuccess :613-638."""
+        failed = [(p, e) for p, _, e in tries if e is not None]
+        if failed:
+            msg = "Secret could not be created due to http errors returned by the following providers: "
+            for p, e in failed:
+                msg += "\n\t" + REQUEST_FOR_ENDPOINT_FAILED_EXCEPTION_MSG % (self.uri(p), e)
+            raise AmphoraClientException(msg)
 
     def create_secret(self, secret: Secret) -> uuid.UUID:
-        odos = self._fan_out(lambda p: p.get_input_masks(secret.secret_id, secret.size()))
+        odos = self._unwrap(self._fan_out(lambda p: p.get_input_masks(secret.secret_id, secret.size())))
         masked = create_masked_input(self.util, secret, odos)
-        self._fan_out(lambda p: p.upload_masked_input(masked))
+        self._check_success(self._fan_out(lambda p: p.upload_masked_input(masked)))
         return secret.secret_id
 
     def get_secret(self, secret_id: uuid.UUID) -> Secret:
         request_id = uuid.uuid4()
-        odos = self._fan_out(lambda p: p.get_secret_share(secret_id, request_id))
+        odos = self._unwrap(self._fan_out(lambda p: p.get_secret_share(secret_id, request_id)))
         data = verify_output_delivery_objects(self.util, odos)
         return Secret(secret_id, list(self.parties[0].secrets[secret_id].tags), data)
 

@@ -88,3 +88,44 @@ def test_upload_without_masks_fails():
     with pytest.raises(A.AmphoraServiceException, match="No input masks found"):
         parties[0].upload_masked_input(mi)
     client.close()
+
+
+def test_party_failures_map_to_client_exceptions():
+    """DefaultAmphoraClientTest.java:237-252,273-288: a failing party surfaces
+    as AmphoraClientException with the reference's message shapes."""
+    import amphora_amd as A
+    client, parties, _, _ = _cluster(2, seed=11)
+    sid = client.create_secret(A.Secret.of([], [42, 24]))
+    orig = parties[1].get_secret_share
+
+    def failing(*a):
+        raise Exception("Call failed")
+
+    parties[1].get_secret_share = failing
+    with pytest.raises(A.AmphoraClientException) as ei:
+        client.get_secret(sid)
+    assert str(ei.value).startswith("Error(s) occurred while processing responses")
+    assert "Call failed" in str(ei.value)
+    parties[1].get_secret_share = orig
+    assert client.get_secret(sid).data == [42, 24]
+    up = parties[1].upload_masked_input
+    parties[1].upload_masked_input = lambda mi: (_ for _ in ()).throw(Exception(500))
+    with pytest.raises(A.AmphoraClientException) as ei:
+        client.create_secret(A.Secret.of([], [7]))
+    assert str(ei.value).endswith('Request for endpoint "loopback://amphora-1" failed: 500')
+    parties[1].upload_masked_input = up
+    client.close()
+
+
+def test_partner_never_answers():
+    """OutputDeliveryServiceTest.java:211-283: the open times out ->
+    AmphoraServiceException("Failed to open values for operation #...")."""
+    import amphora_amd as A
+    from amphora_amd.loopback import AmphoraParty, ExchangeHub
+    rng = random.Random(4)
+    keys = [rng.randrange(P) for _ in range(2)]
+    castor = FakeCastor(P, R, RINV, keys, 4)
+    hub = ExchangeHub(2, timeout_s=0.5)
+    p0 = AmphoraParty(0, P, R, RINV, keys[0], castor, hub)
+    with pytest.raises(A.AmphoraServiceException, match="^Failed to open values for operation #"):
+        p0.get_input_masks(uuid.uuid4(), 10)
