@@ -917,7 +917,8 @@ int amph_base64_decode(amph_ctx* c, const char* in, size_t nchars, uint8_t* out,
                        [&](auto& din, auto& dout, size_t cnt, unsigned long long* ff,
                            const amph::LaunchCfg& lc) {
                          return amph::launch_b64_decode((const char*)din[0], 16 * cnt,
-                                                        (uint8_t*)dout[0], 12 * cnt, ff, lc);
+                                                        (uint8_t*)dout[0], 12 * cnt, ff, lc,
+                                                        false);  // batches never end the text
                        });
   if (st != AMPH_OK && st != AMPH_E_VERIFY) return st;
   unsigned long long tb = amph::kNoFail;

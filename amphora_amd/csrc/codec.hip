@@ -88,7 +88,8 @@ __global__ __launch_bounds__(kMaxBlock) void k_b64_encode(const uint8_t* in, siz
 // nchars % 4 == 0; out_bytes = 3 nchars / 4 - padding; bad = first invalid index
 __global__ __launch_bounds__(kMaxBlock) void k_b64_decode(const char* in, size_t nchars,
                                                       uint8_t* out, size_t out_bytes,
-                                                      unsigned long long* bad) {
+                                                      unsigned long long* bad, size_t ibase,
+                                                      int text_end) {
   const size_t units = (nchars + 15) / 16;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < units; t += stride) {
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(kMaxBlock) void k_b64_decode(const char* in, size_t
       for (int k = 0; k < 4; ++k) {
         const size_t pos = base + 4 * q + k;
         // '=' is legal only in the last two positions of the whole text
-        const bool pad_ok = c[4 * q + k] == '=' && pos >= nchars - 2 &&
+        const bool pad_ok = text_end && c[4 * q + k] == '=' && pos >= nchars - 2 &&
                             (pos == nchars - 1 || in[nchars - 1] == '=');
         v[k] = pad_ok ? 0u : dec6(c[4 * q + k]);
         if (v[k] == 0xFFu && firstbad == 0xFFFFFFFFu) firstbad = (uint32_t)(4 * q + k);
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(kMaxBlock) void k_b64_decode(const char* in, size_t
       o[3 * q + 1] = (g >> 8) & 0xFF;
       o[3 * q + 2] = g & 0xFF;
     }
-    if (firstbad != 0xFFFFFFFFu && (size_t)firstbad < rem) atomicMin(bad, (unsigned long long)(base + firstbad));
+    if (firstbad != 0xFFFFFFFFu && (size_t)firstbad < rem) atomicMin(bad, (unsigned long long)(ibase + base + firstbad));
     const size_t ob = 12 * t;
     uint8_t* op = out + ob;
     if (ob + 12 <= out_bytes && (((uintptr_t)op) & 3) == 0) {
@@ -193,6 +194,77 @@ __global__ __launch_bounds__(kMaxBlock) void k_b64_unwords(const char* in, size_
   }
 }
 
+// Workgroup-staged bulk kernels: a block's contiguous run of input (encode:
+// 12 B x 256 units) or output (decode) moves as fully coalesced 16-B
+// accesses through LDS, each lane still codes its own 12-byte unit from /
+// into LDS (3-dword lane stride: conflict-free).  +46 % encode, +43 % decode
+// over the per-lane kernels (tools/ubench/ubench_b64.hip).  Full blocks
+// only, 16-B aligned buffers; the final unit (partial / '=' padded) and any
+// ragged tail go to the per-lane kernels above.
+constexpr int kB64Block = 256;
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldnt4(const uint4* p) {
+  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__global__ __launch_bounds__(kB64Block) void k_b64_encode_blk(const uint8_t* in, char* out) {
+  __shared__ uint32_t lds[3 * kB64Block];
+  const size_t u0 = (size_t)blockIdx.x * kB64Block, t = u0 + threadIdx.x;
+  const uint4* src = reinterpret_cast<const uint4*>(in + 12 * u0);
+  for (int q = threadIdx.x; q < 3 * kB64Block / 4; q += kB64Block) {
+    const uint4 v = ldnt4(src + q);
+    lds[4 * q] = v.x; lds[4 * q + 1] = v.y; lds[4 * q + 2] = v.z; lds[4 * q + 3] = v.w;
+  }
+  __syncthreads();
+  uint8_t b[12];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const uint32_t x = lds[3 * threadIdx.x + q];
+    b[4 * q] = x & 0xFF; b[4 * q + 1] = (x >> 8) & 0xFF;
+    b[4 * q + 2] = (x >> 16) & 0xFF; b[4 * q + 3] = x >> 24;
+  }
+  uint32_t g[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) g[q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
+  *reinterpret_cast<uint4*>(out + 16 * t) = make_uint4(g[0], g[1], g[2], g[3]);
+}
+
+__global__ __launch_bounds__(kB64Block) void k_b64_decode_blk(const char* in, uint8_t* out,
+                                                             unsigned long long* bad) {
+  __shared__ uint32_t lds[3 * kB64Block];
+  const size_t u0 = (size_t)blockIdx.x * kB64Block, t = u0 + threadIdx.x;
+  const uint4 v = ldnt4(reinterpret_cast<const uint4*>(in) + t);
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t firstbad = 0xFFFFFFFFu;
+  uint8_t o[12];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      d[k] = dec6((w[q] >> (8 * k)) & 0xFF);  // no '=' before the final unit
+      if (d[k] == 0xFFu && firstbad == 0xFFFFFFFFu) firstbad = 4 * q + k;
+    }
+    const uint32_t g = (d[0] << 18) | (d[1] << 12) | (d[2] << 6) | d[3];
+    o[3 * q] = (g >> 16) & 0xFF;
+    o[3 * q + 1] = (g >> 8) & 0xFF;
+    o[3 * q + 2] = g & 0xFF;
+  }
+  if (firstbad != 0xFFFFFFFFu) atomicMin(bad, (unsigned long long)(16 * t + firstbad));
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    lds[3 * threadIdx.x + q] =
+        o[4 * q] | (o[4 * q + 1] << 8) | (o[4 * q + 2] << 16) | ((uint32_t)o[4 * q + 3] << 24);
+  __syncthreads();
+  uint4* dst = reinterpret_cast<uint4*>(out + 12 * u0);
+  for (int q = threadIdx.x; q < 3 * kB64Block / 4; q += kB64Block)
+    dst[q] = make_uint4(lds[4 * q], lds[4 * q + 1], lds[4 * q + 2], lds[4 * q + 3]);
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 unsigned grid_n(size_t n, const LaunchCfg& c) {
   size_t g = (n + c.block - 1) / c.block;
   if (c.grid_cap > 0 && g > (size_t)c.grid_cap) g = (size_t)c.grid_cap;
@@ -202,17 +274,35 @@ unsigned grid_n(size_t n, const LaunchCfg& c) {
 
 }  // namespace
 
+// Bulk: full 256-unit blocks that end before the final unit, when both
+// buffers are 16-B aligned; the rest: the per-lane kernel on the tail.
 hipError_t launch_b64_encode(const uint8_t* in, size_t nbytes, char* out, const LaunchCfg& c) {
   if (nbytes == 0) return hipSuccess;
-  AMPH_LAUNCH(k_b64_encode, dim3(grid_n((nbytes + 11) / 12, c)), dim3(c.block), c, in, nbytes, out);
+  const size_t units = (nbytes + 11) / 12;
+  const size_t nblk = aligned16(in) && aligned16(out) ? (units - 1) / kB64Block : 0;
+  const size_t done = nblk * kB64Block;
+  LaunchCfg c0 = c, c1 = c;
+  c0.ev_stop = nullptr;
+  c1.ev_start = nullptr;
+  if (nblk) AMPH_LAUNCH(k_b64_encode_blk, dim3((unsigned)nblk), dim3(kB64Block), c0, in, out);
+  AMPH_LAUNCH(k_b64_encode, dim3(grid_n(units - done, c)), dim3(c.block), nblk ? c1 : c, in + 12 * done,
+              nbytes - 12 * done, out + 16 * done);
   return hipGetLastError();
 }
 
 hipError_t launch_b64_decode(const char* in, size_t nchars, uint8_t* out, size_t out_bytes,
-                             unsigned long long* bad, const LaunchCfg& c) {
+                             unsigned long long* bad, const LaunchCfg& c, bool text_end) {
   if (nchars == 0) return hipSuccess;
-  AMPH_LAUNCH(k_b64_decode, dim3(grid_n((nchars + 15) / 16, c)), dim3(c.block), c, in, nchars, out,
-              out_bytes, bad);
+  const size_t units = (nchars + 15) / 16;
+  const size_t nblk = aligned16(in) && aligned16(out) ? (units - 1) / kB64Block : 0;
+  const size_t done = nblk * kB64Block;
+  LaunchCfg c0 = c, c1 = c;
+  c0.ev_stop = nullptr;
+  c1.ev_start = nullptr;
+  if (nblk) AMPH_LAUNCH(k_b64_decode_blk, dim3((unsigned)nblk), dim3(kB64Block), c0, in, out, bad);
+  AMPH_LAUNCH(k_b64_decode, dim3(grid_n(units - done, c)), dim3(c.block), nblk ? c1 : c, in + 16 * done,
+              nchars - 16 * done, out + 12 * done, out_bytes - 12 * done, bad, 16 * done,
+              (int)text_end);
   return hipGetLastError();
 }
 

@@ -84,8 +84,9 @@ hipError_t launch_mask_words(const uint4* secrets, const uint4* masks, size_t wo
 
 // base64 wire codec (codec.hip): standard alphabet, '=' padding, no line breaks.
 hipError_t launch_b64_encode(const uint8_t* in, size_t nbytes, char* out, const LaunchCfg& c);
+// text_end: the range ends the text, so '=' may pad its last two chars
 hipError_t launch_b64_decode(const char* in, size_t nchars, uint8_t* out, size_t out_bytes,
-                             unsigned long long* bad, const LaunchCfg& c);
+                             unsigned long long* bad, const LaunchCfg& c, bool text_end = true);
 hipError_t launch_b64_words(const uint4* in, size_t words, char* out, const LaunchCfg& c);
 hipError_t launch_b64_unwords(const char* in, size_t words, uint4* out, unsigned long long* bad,
                               const LaunchCfg& c);

@@ -276,3 +276,37 @@ def test_exchange_decode_count_and_brackets(ctx):
     m, n = ctx.exchange_decode(b"[]", 0)
     assert m.shape == (0, 2, 16)
     assert ctx.exchange_encode(np.zeros((0, 2, 16), np.uint8), np.zeros((0, 2), np.uint8)) == b"[]"
+
+
+def test_base64_padding_only_at_text_end(ctx):
+    """'=' in the last chars of an interior host batch is an illegal character,
+    not padding (the batch is not the end of the text)."""
+    raw = np.random.default_rng(9).integers(0, 256, 3 * 40_000, dtype=np.uint8).tobytes()
+    enc = bytearray(base64.b64encode(raw))
+    enc[16 * 4096 - 1] = ord("=")
+    ctx.set_batch_words(4096)  # decode batches of 4096 16-char units
+    try:
+        with pytest.raises(ValueError, match="index %d" % (16 * 4096 - 1)):
+            ctx.base64_decode(bytes(enc))
+    finally:
+        ctx.set_batch_words(4 << 20)
+
+
+@pytest.mark.parametrize("off", [0, 1, 4, 8])
+def test_base64_device_alignment(ctx, off):
+    """Bulk (LDS-staged) and per-lane kernels agree for aligned and
+    misaligned device buffers, with a bad character in the bulk range."""
+    import torch
+    raw = np.random.default_rng(off).integers(0, 256, 3 * 100_003 + 2, dtype=np.uint8).tobytes()
+    exp = base64.b64encode(raw)
+    t = torch.zeros(len(raw) + 16, dtype=torch.uint8, device="cuda")
+    t[off:off + len(raw)] = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
+    enc = ctx.base64_encode(t[off:off + len(raw)])
+    assert enc.cpu().numpy().tobytes() == exp
+    e2 = torch.zeros(len(exp) + 16, dtype=torch.uint8, device="cuda")
+    e2[off:off + len(exp)] = enc
+    dec, bad = ctx.base64_decode(e2[off:off + len(exp)])
+    assert dec.cpu().numpy().tobytes() == raw and int(bad.item()) == 0x7F7F7F7F7F7F7F7F
+    e2[off + 50_001] = ord("?")
+    _, bad = ctx.base64_decode(e2[off:off + len(exp)])
+    assert int(bad.item()) == 50_001
