@@ -235,6 +235,9 @@ def main():
     local = 0 if a.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     distributed = world > 1 or a.dist
+    if a.gpus != world and rank == 0:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d; launch one process per GPU with "
+              "torch.distributed.run (measuring %d)" % (a.gpus, world, world), file=sys.stderr)
     if distributed:
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
