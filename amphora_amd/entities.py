@@ -28,6 +28,10 @@ class IllegalArgumentException(ValueError):
     """java.lang.IllegalArgumentException as thrown on the path."""
 
 
+class NullPointerException(TypeError):
+    """java.lang.NullPointerException from lombok @NonNull, same message."""
+
+
 class AmphoraServiceException(RuntimeError):
     """AmphoraServiceException.java:16-37."""
 
@@ -82,9 +86,19 @@ class MaskedInputData:
 
 @dataclass
 class MaskedInput:
+    """MaskedInput.java:25-62: secretId and data non-null; null tags become an
+    empty list (MaskedInputTest.java)."""
     secret_id: uuid.UUID
     data: List[MaskedInputData]
     tags: list = field(default_factory=list)
+
+    def __post_init__(self):
+        for name in ("secret_id", "data"):
+            if getattr(self, name) is None:
+                raise NullPointerException("%s is marked non-null but is null"
+                                           % ("secretId" if name == "secret_id" else name))
+        if self.tags is None:
+            self.tags = []
 
 
 INVALID_LENGTH_EXCEPTION_MSG = "Length of a SecretShare's data must e a multiple of %s bytes!"

@@ -65,6 +65,15 @@ def test_entities_invariants(native):
         E.MaskedInputData.of(b"\0" * 15)
     with pytest.raises(E.IllegalArgumentException, match="multiple of 32"):
         E.SecretShare(None, b"\0" * 48)
+    # MaskedInputTest.java: null id rejected, null tags -> empty list
+    with pytest.raises(E.NullPointerException, match="^secretId is marked non-null but is null$"):
+        E.MaskedInput(None, [], [])
+    import uuid
+    sid = uuid.UUID("80fbba1b-3da8-4b1e-8a2c-cebd65229fad")
+    mi = E.MaskedInput(sid, [E.MaskedInputData.of(bytes(16))], None)
+    assert mi.secret_id == sid and mi.tags == []
+    with pytest.raises(E.IllegalArgumentException, match="^Length of a Masked Input value has to be 16 bytes.$"):
+        E.MaskedInputData.of(bytes(15))
 
 
 def test_name_uuid(native):

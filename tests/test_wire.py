@@ -71,6 +71,10 @@ def test_vss_json_missing_field(ctx):
     invalid = re.sub(r'"rShares" :\s"\S+",', "", _vss_expected(), count=1)
     with pytest.raises(A.IllegalArgumentException, match="rShares is marked non-null but is null"):
         wire.vss_from_json(ctx, invalid)
+    # VerifiableSecretTest.java:102-111: the Metadata side
+    invalid = re.sub(r'"secretId" :\s"\S+",', "", _vss_expected(), count=1)
+    with pytest.raises(A.IllegalArgumentException, match="secretId is marked non-null but is null"):
+        wire.vss_from_json(ctx, invalid)
 
 
 @pytest.mark.parametrize("mode", ["host", "device"])
