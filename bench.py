@@ -39,6 +39,12 @@ def kbytes(kernel: str, n: int) -> int:
     return {"k_rv": 80 * n + 16, "k_mask": 80 * n + 32}[kernel]
 
 
+def config_name(words: int, parties: int) -> str:
+    """BASELINE.json config a device-resident run corresponds to (per GPU)."""
+    return {(1 << 20, 2): "C2", (1 << 24, 3): "C3", (1 << 26, 2): "C4 size"}.get(
+        (words, parties), "custom")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -349,8 +355,9 @@ def main():
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u128 mod-p (4x u32 limbs)",
             "data": "synthetic: device-generated honest %d-party ODOs + secrets (seeded)" % n,
-            "config": {"workload": "C2: K_MASK (share-encode) + K_RV (recombine+verify), "
-                                   "%d words per GPU, %d parties, p = 2^127 < p < 2^128 test prime" % (W, n),
+            "config": {"workload": "%s: K_MASK (share-encode) + K_RV (recombine+verify), "
+                                   "%d words per GPU, %d parties, p = 2^127 < p < 2^128 test prime"
+                                   % (config_name(W, n), W, n),
                        "words_per_gpu": W, "parties": n, "parallelism": "dp%d" % world},
             "verified": ok,
             "kernels_ms": {k: round(v, 5) for k, v in kern.items()},
