@@ -39,7 +39,6 @@ constexpr int kXBlock = 256;      // pairs per workgroup (encode)
 constexpr int kXEntry = 92;       // max entry: {"a":-<39 digits>,"b":-<39 digits>},
 constexpr int kScanBlock = 1024;  // elements per workgroup of the scan passes
 constexpr int kDecBytes = 32;     // text bytes per lane (decode)
-constexpr int kDecBlock = 256;
 constexpr uint64_t kE9 = 1000000000ull;
 
 __device__ __forceinline__ uint32_t divmod_e9(uint32_t (&v)[4]) {
@@ -219,61 +218,108 @@ __global__ __launch_bounds__(kXBlock) void k_xenc_write(const uint4* mag, const 
 }
 
 // ---- decode -----------------------------------------------------------------------
+// The text is addressed in "virtual" coordinates: v = byte offset from the
+// 16-byte-aligned address at or below the text, so every 16-byte chunk load
+// is aligned; virtual bytes before the text (v < mis) and after it (v >= L)
+// read as ' ' (JSON whitespace).  A chunk that holds a real byte lies in the
+// same 16-byte granule as that byte, so it never crosses a page.
+struct Text {
+  const uint8_t* al;  // aligned base
+  size_t mis, L;      // L = mis + len
+  __device__ __forceinline__ uint32_t operator[](size_t v) const {
+    return v - mis < L - mis ? al[v] : (uint32_t)' ';
+  }
+  __device__ __forceinline__ uint4 chunk(long long v) const {  // 16-aligned v
+    if (v + 16 <= (long long)mis || v >= (long long)L) return make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+    uint4 c = *reinterpret_cast<const uint4*>(al + v);
+    if (v < (long long)mis || v + 16 > (long long)L) {
+      uint32_t w[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const long long x = v + j;
+        if (x < (long long)mis || x >= (long long)L)
+          w[j >> 2] = (w[j >> 2] & ~(0xFFu << (8 * (j & 3)))) | (0x20u << (8 * (j & 3)));
+      }
+      c = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    return c;
+  }
+};
+
 __device__ __forceinline__ bool is_digit(uint32_t c) { return c - '0' < 10u; }
 __device__ __forceinline__ bool is_ws(uint32_t c) {
   return c == ' ' || c == '\n' || c == '\r' || c == '\t';
 }
-__device__ __forceinline__ bool num_char(uint32_t c) {
-  return is_digit(c) || c == '-' || c == '+' || c == '.' || c == 'e' || c == 'E';
+
+// SWAR byte classes on 4 text bytes: bit 7 of byte j set iff byte j is in the class.
+__device__ __forceinline__ uint32_t swar_digit(uint32_t w) {
+  const uint32_t lo = w & 0x7F7F7F7Fu;
+  return (lo + 0x50505050u) & ~(lo + 0x46464646u) & ~w & 0x80808080u;  // 0x30 <= b <= 0x39
+}
+__device__ __forceinline__ uint32_t swar_eq(uint32_t w, uint32_t ch) {
+  const uint32_t y = w ^ (ch * 0x01010101u);
+  return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
+}
+// bytes that continue a JSON number token (digits, sign, fraction, exponent)
+__device__ __forceinline__ uint32_t swar_numchar(uint32_t w) {
+  return swar_digit(w) | swar_eq(w, '-') | swar_eq(w, '+') | swar_eq(w, '.') | swar_eq(w, 'e') |
+         swar_eq(w, 'E');
 }
 
-// Bit j of the result: byte base+j starts a number (a digit or '-' whose
-// predecessor is not part of a number token).
-__device__ __forceinline__ uint32_t start_mask(const uint8_t* t, size_t len, size_t base) {
-  uint8_t b[kDecBytes + 1];
-  b[0] = base > 0 ? t[base - 1] : ' ';
-  if (base + kDecBytes <= len && (((uintptr_t)(t + base)) & 15) == 0) {
-    const uint4* p = reinterpret_cast<const uint4*>(t + base);
-#pragma unroll
-    for (int q = 0; q < kDecBytes / 16; ++q) {
-      const uint4 v = p[q];
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 16; ++j) b[1 + 16 * q + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < kDecBytes; ++j) b[1 + j] = base + j < len ? t[base + j] : ' ';
-  }
+// Number starts in 32 text bytes (8 dwords): a digit or '-' whose predecessor
+// does not continue a number.  prev_nc: numchar flag of the byte before (bit 31).
+// Returns one bit per byte.
+__device__ __forceinline__ uint32_t starts32(const uint32_t (&w)[8], uint32_t prev_nc) {
   uint32_t m = 0;
 #pragma unroll
-  for (int j = 0; j < kDecBytes; ++j) {
-    const uint32_t c = b[1 + j];
-    m |= (uint32_t)((is_digit(c) || c == '-') && !num_char(b[j])) << j;
+  for (int d = 0; d < 8; ++d) {
+    const uint32_t nc = swar_numchar(w[d]);
+    const uint32_t pnc = (nc << 8) | (prev_nc >> 24);
+    const uint32_t s = ((swar_digit(w[d]) | swar_eq(w[d], '-')) & ~pnc & 0x80808080u) >> 7;
+    m |= ((s | (s >> 7) | (s >> 14) | (s >> 21)) & 0xFu) << (4 * d);
+    prev_nc = nc;
   }
   return m;
 }
 
-__global__ __launch_bounds__(kDecBlock) void k_xdec_count(const uint8_t* t, size_t len,
-                                                      uint64_t* bsum) {
-  const size_t base = ((size_t)blockIdx.x * kDecBlock + threadIdx.x) * kDecBytes;
-  const uint64_t c = base < len ? __popc(start_mask(t, len, base)) : 0;
+constexpr int kDecBlock = 512;                         // threads per workgroup
+constexpr size_t kDecSpan = (size_t)kDecBlock * kDecBytes;  // 16 KiB of text per workgroup
+constexpr int kWinPad = 256;                           // window context either side
+constexpr int kWin = (int)kDecSpan + 2 * kWinPad;      // staged bytes
+
+// Pass 1: number starts per workgroup.
+__global__ __launch_bounds__(kDecBlock) void k_xdec_count(Text t, uint64_t* bsum) {
+  const size_t base = (size_t)blockIdx.x * kDecSpan + (size_t)threadIdx.x * kDecBytes;
+  const uint4 c0 = t.chunk((long long)base), c1 = t.chunk((long long)base + 16);
+  const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  // numchar flag of the byte before: the previous lane's last dword (lane 0: a load)
+  const uint32_t prev_last = __shfl_up(w[7], 1, 64);
+  const uint32_t pb = __lane_id() == 0 ? (base ? t[base - 1] : (uint32_t)' ') << 24 : prev_last;
+  const uint64_t cnt = __popc(starts32(w, swar_numchar(pb)));
   uint64_t total;
-  block_excl_scan(c, &total);
+  block_excl_scan(cnt, &total);
   if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-// The workgroup's text window (its 8 KiB plus 256 B either side) staged in
-// LDS; bytes outside it (long whitespace runs) come from global memory.
+// The workgroup's 16 KiB plus kWinPad bytes either side, staged in LDS;
+// bytes outside it (long whitespace runs) come from global memory.
 struct Window {
-  const uint8_t* t;
+  Text t;
   const uint8_t* lds;
-  size_t w0, w1;
+  size_t w0;  // virtual offset of lds[0] (may be "negative": wraps, never in range then)
   __device__ __forceinline__ uint32_t operator[](size_t x) const {
-    return x - w0 < w1 - w0 ? lds[x - w0] : t[x];
+    return x - w0 < (size_t)kWin ? (uint32_t)lds[x - w0] : t[x];
+  }
+  // 4 bytes starting at x (little-endian)
+  __device__ __forceinline__ uint32_t word(size_t x) const {
+    const size_t o = x - w0;
+    if (o < (size_t)kWin) {  // the window has one spare dword past kWin
+      const uint32_t* l32 = reinterpret_cast<const uint32_t*>(lds);
+      return __builtin_amdgcn_alignbyte(l32[(o >> 2) + 1], l32[o >> 2], (uint32_t)(o & 3));
+    }
+    return t[x] | (t[x + 1] << 8) | (t[x + 2] << 16) | (t[x + 3] << 24);
   }
 };
-constexpr int kWinPad = 256;
 
 template <class T>
 __device__ __forceinline__ size_t skip_ws_back(const T& t, size_t q) {  // q: index+1
@@ -295,101 +341,176 @@ __device__ __forceinline__ uint32_t key_before(const T& t, size_t x, size_t* q) 
   return k;
 }
 
-__global__ __launch_bounds__(kDecBlock) void k_xdec_parse(const uint8_t* text, size_t len,
-                                                      const uint64_t* bscan, size_t nvals,
-                                                      uint4* mag, uint8_t* neg,
+__device__ __forceinline__ void fold(uint32_t (&v)[4], uint32_t mul, uint32_t add, bool& ovf) {
+  uint64_t carry = add;  // v = v * mul + add
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t s = (uint64_t)v[i] * mul + carry;
+    v[i] = (uint32_t)s;
+    carry = s >> 32;
+  }
+  ovf |= carry != 0;
+}
+
+// Pass 3: each workgroup finds its number starts again (from LDS), scans
+// them to global number indices and lists their positions in LDS; then its
+// lanes take ONE NUMBER EACH, consecutive numbers on consecutive lanes (so a
+// wave's trip counts match), read the digits four at a time (SWAR) and check
+// the grammar around the number:
+//   member 0: '[' ws | '}' ws ',' ws (after the previous pair's digits), then
+//             '{' ws "k" ws ':' ws NUM ws ','
+//   member 1: ',' ws "k" ws ':' ws NUM ws '}'  (last pair: ws ']' ws EOF)
+// Phase 1 does each number's own checks and records in LDS where its digits
+// end, its key, and (member 1) where the text before its ',' ends; phase 2
+// ties each member 1 to the member 0 before it (same ',', other key), so
+// together they cover every byte of a well-formed array.  A well-formed text
+// has at most kMaxStarts numbers per 16 KiB ({"a":1,"b":2}, = 14 bytes per 2);
+// a start beyond that is reported as malformed.
+constexpr int kMaxStarts = 2560;
+
+__global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint64_t* bscan,
+                                                      size_t nvals, uint4* mag, uint8_t* neg,
                                                       unsigned long long* bad) {
-  __shared__ uint8_t win[kDecBlock * kDecBytes + 2 * kWinPad];
-  const size_t b0 = (size_t)blockIdx.x * kDecBlock * kDecBytes;
-  const size_t w0 = b0 > (size_t)kWinPad ? b0 - kWinPad : 0;
-  const size_t w1 = min(len, b0 + (size_t)kDecBlock * kDecBytes + kWinPad);
-  for (size_t i = threadIdx.x; i < w1 - w0; i += kDecBlock) win[i] = text[w0 + i];
-  const Window t{text, win, w0, w1};
-  const size_t base = b0 + (size_t)threadIdx.x * kDecBytes;
-  uint32_t m = base < len ? start_mask(text, len, base) : 0;
+  __shared__ uint4 win4[kWin / 16 + 1];
+  __shared__ uint16_t pos[kMaxStarts];   // start, relative to b0
+  __shared__ uint16_t endp[kMaxStarts];  // one past the last digit, relative to w0
+  __shared__ uint16_t comma[kMaxStarts]; // member 1: one past the last byte before its ',', rel. w0
+  __shared__ uint8_t keyc[kMaxStarts];   // 'a' / 'b', 0 if the number failed its own checks
+  const size_t b0 = (size_t)blockIdx.x * kDecSpan;
+  const long long w0 = (long long)b0 - kWinPad;
+  for (int c = threadIdx.x; c < kWin / 16 + 1; c += kDecBlock) win4[c] = text.chunk(w0 + 16LL * c);
+  __syncthreads();
+  const uint8_t* win = reinterpret_cast<const uint8_t*>(win4);
+  const Window t{text, win, (size_t)w0};
+  const int lo = kWinPad + kDecBytes * threadIdx.x;  // this lane's 32 bytes in the window
+  const uint4 c0 = win4[lo / 16], c1 = win4[lo / 16 + 1];
+  const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  uint32_t m = starts32(w, swar_numchar((uint32_t)win[lo - 1] << 24));
   uint64_t total;
-  uint64_t g = bscan[blockIdx.x] + block_excl_scan(__popc(m), &total);  // (its barriers also publish win)
-  for (; m; m &= m - 1, ++g) {
-    const size_t x = base + __ffs(m) - 1;
+  const uint64_t first = block_excl_scan(__popc(m), &total);
+  for (int k = (int)first; m; m &= m - 1, ++k) {
+    const int at = kDecBytes * threadIdx.x + __ffs(m) - 1;
+    if (k < kMaxStarts) pos[k] = (uint16_t)at;
+    else if (k == kMaxStarts) atomicMin(bad, (unsigned long long)(b0 + at - text.mis));
+  }
+  __syncthreads();
+  const uint32_t nloc = (uint32_t)min(total, (uint64_t)kMaxStarts);
+  const uint64_t gbase = bscan[blockIdx.x];
+  // phase 1: own checks + value
+  for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
+    const size_t x = b0 + pos[idx];
+    const uint64_t g = gbase + idx;
+    const bool first_m = (g & 1) == 0;
     size_t q = 0;
     const uint32_t key = key_before(t, x, &q);
-    bool ok = key != 0 && g < nvals;
-    // member 0 follows '{' (itself after '[' or ','), member 1 follows ','
-    const bool first = (g & 1) == 0;
-    if (ok) {
-      if (first) {
-        ok = q > 0 && t[q - 1] == '{';
-        if (ok) {
-          const size_t r = skip_ws_back(t, q - 1);
-          ok = r > 0 && (t[r - 1] == '[' || t[r - 1] == ',');
-        }
+    bool ok = key != 0 && g < nvals && q > 0;
+    size_t cm = 0;
+    if (ok && first_m) {  // '{' ws then '[' ws BOF (first pair) or '}' ws ',' ws after a digit
+      ok = t[q - 1] == '{';
+      const size_t r = skip_ws_back(t, q - 1);
+      if (g == 0) {
+        ok = ok && r > 0 && t[r - 1] == '[' && skip_ws_back(t, r - 1) == 0;
       } else {
-        ok = q > 0 && t[q - 1] == ',';
-        if (ok) {  // the other member: number, then its key, then '{'
-          size_t r = skip_ws_back(t, q - 1);
-          while (r > 0 && is_digit(t[r - 1])) --r;
-          if (r > 0 && t[r - 1] == '-') --r;
-          size_t q0 = 0;
-          const uint32_t k0 = key_before(t, r, &q0);
-          ok = k0 != 0 && k0 != key && q0 > 0 && t[q0 - 1] == '{';
-        }
+        ok = ok && r > 0 && t[r - 1] == ',';
+        const size_t r2 = ok ? skip_ws_back(t, r - 1) : 0;
+        ok = ok && r2 > 0 && t[r2 - 1] == '}';
+        const size_t r3 = ok ? skip_ws_back(t, r2 - 1) : 0;
+        ok = ok && r3 > 0 && is_digit(t[r3 - 1]);
       }
+    } else if (ok) {  // ',' ws before the key
+      ok = t[q - 1] == ',';
+      cm = skip_ws_back(t, q - 1);
     }
-    // the number: optional '-', 1..39 digits, value < 2^128
+    // the number: optional '-', 1..39 digits without a leading zero, value < 2^128
     size_t p = x;
     const bool minus = t[p] == '-';
     p += minus;
+    const bool lead0 = t[p] == '0';
     uint32_t v[4] = {0, 0, 0, 0};
     int nd = 0;
-    uint32_t chunk = 0, cmul = 1;
     bool ovf = false;
-    auto fold = [&](uint32_t mul, uint32_t add) {  // v = v * mul + add
-      uint64_t carry = add;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint64_t s = (uint64_t)v[i] * mul + carry;
-        v[i] = (uint32_t)s;
-        carry = s >> 32;
+    for (;;) {
+      const uint32_t b = t.word(p);
+      const uint32_t nondig = ~swar_digit(b) & 0x80808080u;
+      const int k = nondig ? (__builtin_ctz(nondig) >> 3) : 4;
+      if (k > 0) {  // the k leading digits as a k-digit value
+        uint32_t d = (b - 0x30303030u) << (8 * (4 - k));
+        d = d * 10u + (d >> 8);
+        fold(v, k == 4 ? 10000u : k == 3 ? 1000u : k == 2 ? 100u : 10u, (d & 0xFFu) * 100u + ((d >> 16) & 0xFFu), ovf);
+        nd += k;
+        p += k;
       }
-      ovf |= carry != 0;
-    };
-    while (p < len && is_digit(t[p]) && nd <= 39) {
-      chunk = chunk * 10u + (t[p] - '0');
-      cmul *= 10u;
-      if (cmul == 1000000000u) {
-        fold(cmul, chunk);
-        chunk = 0;
-        cmul = 1;
-      }
-      ++p;
-      ++nd;
+      if (k < 4 || nd > 39) break;
     }
-    if (cmul > 1) fold(cmul, chunk);
-    ok = ok && nd > 0 && nd <= 39 && !ovf;
+    ok = ok && nd > 0 && nd <= 39 && !ovf && !(lead0 && nd > 1);
+    const size_t dend = p;
     if (ok) {  // the token ends the member: ws then ',' (member 0) or '}' (member 1)
-      while (p < len && is_ws(t[p])) ++p;
-      ok = p < len && t[p] == (first ? ',' : '}');
+      while (p < text.L && is_ws(t[p])) ++p;
+      ok = p < text.L && t[p] == (first_m ? ',' : '}');
+      if (ok && g + 1 == nvals) {  // the last pair closes the array: '}' ws ']' ws EOF
+        ++p;
+        while (p < text.L && is_ws(t[p])) ++p;
+        ok = p < text.L && t[p] == ']';
+        ++p;
+        while (ok && p < text.L && is_ws(t[p])) ++p;
+        ok = ok && p == text.L;
+      }
     }
+    endp[idx] = (uint16_t)(dend - (size_t)w0);
+    comma[idx] = (uint16_t)(cm - (size_t)w0);
+    keyc[idx] = ok ? (uint8_t)key : 0;
     if (!ok) {
-      atomicMin(bad, (unsigned long long)x);
+      atomicMin(bad, (unsigned long long)(x - text.mis));
       continue;
     }
     const size_t slot = (g & ~(uint64_t)1) + (key == 'b');
     mag[slot] = make_uint4(v[0], v[1], v[2], v[3]);
     neg[slot] = minus && (v[0] | v[1] | v[2] | v[3]) != 0;
   }
+  __syncthreads();
+  // phase 2: member 1 follows its member 0: the same ',', the other key
+  for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
+    const uint64_t g = gbase + idx;
+    const uint32_t key = keyc[idx];
+    if ((g & 1) == 0 || key == 0) continue;
+    bool ok;
+    if (idx > 0) {
+      ok = comma[idx] == endp[idx - 1] && keyc[idx - 1] != 0 && keyc[idx - 1] != key;
+    } else {  // member 0 sits in the previous span: walk back over its digits
+      const size_t x = b0 + pos[idx];
+      size_t q = 0;
+      key_before(t, x, &q);
+      size_t r = skip_ws_back(t, q - 1);
+      while (r > 0 && is_digit(t[r - 1])) --r;
+      if (r > 0 && t[r - 1] == '-') --r;
+      size_t q0 = 0;
+      const uint32_t k0 = key_before(t, r, &q0);
+      ok = k0 != 0 && k0 != key && q0 > 0 && t[q0 - 1] == '{';
+    }
+    if (!ok) atomicMin(bad, (unsigned long long)(b0 + pos[idx] - text.mis));
+  }
 }
 
-// the array holds exactly nvals numbers and is bracketed
-__global__ void k_xdec_check(const uint8_t* t, size_t len, const uint64_t* bscan, size_t nb,
-                             size_t nvals, unsigned long long* bad) {
-  size_t a = 0;
-  while (a < len && is_ws(t[a])) ++a;
-  size_t z = len;
-  while (z > 0 && is_ws(t[z - 1])) --z;
-  if (a >= len || t[a] != '[') atomicMin(bad, (unsigned long long)a);
-  else if (z == 0 || t[z - 1] != ']') atomicMin(bad, (unsigned long long)(z ? z - 1 : 0));
-  else if (bscan[nb] != nvals) atomicMin(bad, (unsigned long long)len);
+// The array holds exactly nvals numbers and is bracketed; an empty array
+// holds nothing but whitespace (with numbers, the lanes above check the rest).
+__global__ __launch_bounds__(256) void k_xdec_check(Text t, const uint64_t* bscan, size_t nb,
+                                                    size_t nvals, unsigned long long* bad) {
+  __shared__ size_t az[2];
+  if (threadIdx.x == 0) {
+    size_t a = t.mis;
+    while (a < t.L && is_ws(t[a])) ++a;
+    size_t z = t.L;
+    while (z > t.mis && is_ws(t[z - 1])) --z;
+    if (a >= t.L || t[a] != '[') atomicMin(bad, (unsigned long long)(a - t.mis));
+    else if (z <= a + 1 || t[z - 1] != ']') atomicMin(bad, (unsigned long long)(z > t.mis ? z - 1 - t.mis : 0));
+    else if (bscan[nb] != nvals) atomicMin(bad, (unsigned long long)(t.L - t.mis));
+    az[0] = a + 1;
+    az[1] = z > t.mis ? z - 1 : t.mis;
+  }
+  __syncthreads();
+  if (nvals == 0)
+    for (size_t i = az[0] + threadIdx.x; i < az[1]; i += blockDim.x)
+      if (!is_ws(t[i])) atomicMin(bad, (unsigned long long)(i - t.mis));
 }
 
 unsigned blocks_of(size_t n, size_t per) { return (unsigned)((n + per - 1) / per); }
@@ -440,23 +561,27 @@ hipError_t launch_exchange_encode(const uint4* mag, const uint8_t* neg, size_t n
 }
 
 size_t xdec_scratch_bytes(size_t len) {
-  return 8 * ((size_t)blocks_of(len ? len : 1, (size_t)kDecBlock * kDecBytes) + 1);
+  const size_t nb = blocks_of(len + 16, kDecSpan);
+  return 8 * (nb + 1) + 8 * ((size_t)blocks_of(nb, kScanBlock) + 1);
 }
 
 hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, uint4* mag,
                                   uint8_t* neg, unsigned long long* bad, void* scratch,
                                   const LaunchCfg& c) {
+  const size_t mis = (uintptr_t)text & 15;
+  const Text t{reinterpret_cast<const uint8_t*>(text) - mis, mis, mis + len};
+  const size_t nb = blocks_of(t.L ? t.L : 1, kDecSpan);
   uint64_t* bscan = static_cast<uint64_t*>(scratch);
-  const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
-  const unsigned nb = blocks_of(len ? len : 1, (size_t)kDecBlock * kDecBytes);
+  uint64_t* bsum = bscan + nb + 1;
   LaunchCfg c0 = c, cm = c, c1 = c;
   c0.ev_stop = nullptr;
   cm.ev_start = cm.ev_stop = nullptr;
   c1.ev_start = nullptr;
-  AMPH_LAUNCH(k_xdec_count, dim3(nb), dim3(kDecBlock), c0, t, len, bscan);
-  AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), cm, bscan, (size_t)nb);
-  AMPH_LAUNCH(k_xdec_parse, dim3(nb), dim3(kDecBlock), cm, t, len, bscan, 2 * npairs, mag, neg, bad);
-  AMPH_LAUNCH(k_xdec_check, dim3(1), dim3(1), c1, t, len, bscan, (size_t)nb, 2 * npairs, bad);
+  AMPH_LAUNCH(k_xdec_count, dim3((unsigned)nb), dim3(kDecBlock), c0, t, bscan);
+  hipError_t e = scan_u64(bscan, nb, bsum, cm);
+  if (e != hipSuccess) return e;
+  AMPH_LAUNCH(k_xdec_parse, dim3((unsigned)nb), dim3(kDecBlock), cm, t, bscan, 2 * npairs, mag, neg, bad);
+  AMPH_LAUNCH(k_xdec_check, dim3(1), dim3(256), c1, t, bscan, nb, 2 * npairs, bad);
   return hipGetLastError();
 }
 

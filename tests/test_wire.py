@@ -256,6 +256,14 @@ def test_exchange_decode_whitespace_and_order(ctx):
     assert np.array_equal(m3, mag)
 
 
+_JSON_BUT_NOT_FACTORPAIRS = {
+    b'[{"a":1,"b":2},{"a":1.5,"b":2}]', b'[{"a":1,"b":2},{"a":1e5,"b":2}]',
+    b'[{"a":1,"b":2},{"a":1,"a":2}]', b'[{"a":1,"b":2},{"a":1,"c":2}]',
+    b'[{"a":1,"b":2},{"a":"1","b":2}]', b'[{"a":1,"b":2},{"a":1,"b":2,"a":3}]',
+    b'[{"a":1,"b":2},{"a":340282366920938463463374607431768211456,"b":2}]',
+}
+
+
 @pytest.mark.parametrize("text,where", [
     (b'[{"a":1,"b":2},{"a":1.5,"b":2}]', 20),
     (b'[{"a":1,"b":2},{"a":1e5,"b":2}]', 20),
@@ -266,10 +274,61 @@ def test_exchange_decode_whitespace_and_order(ctx):
     (b'[{"a":1,"b":2} {"a":1,"b":2}]', 20),
     (b'[{"a":1,"b":2},{"a":340282366920938463463374607431768211456,"b":2}]', 20),
     (b'[{"a":1,"b":2},{"a":--1,"b":2}]', 20),
+    (b'[{"a":1,"b":2},{"a":01,"b":2}]', 20),   # leading zero (Jackson's default rejects it)
+    (b'[{"a":1,"b":2},{"a":-00,"b":2}]', 20),
+    (b'[{"a":1,"b":2}x,{"a":1,"b":2}]', 21),    # bytes between objects
+    (b'[{"a":1,"b":2}}, {"a":1,"b":2}]', 22),
+    (b'[{"a":1,"b":2},,{"a":1,"b":2}]', 21),
+    (b'[{"a":1,"b":2},{"a":1,"b":2}x]', 26),    # bytes before the closing bracket
+    (b'[{"a":1,"b":2},{"a":1,"b":2}]]', 26),
+    (b'[{"a":1,"b":2},{"a":1,"b":2}] [', 26),   # bytes after the array
 ])
 def test_exchange_decode_rejects(ctx, text, where):
+    """Every byte of the array is checked against the FactorPair grammar; the
+    reported offset is the number whose surroundings break it.  Texts that are
+    not JSON at all are rejected by Python's json module too (standing in for
+    Jackson); the rest are JSON but not a FactorPair list of integers."""
+    try:
+        json.loads(text)
+        grammar_ok = True
+    except ValueError:
+        grammar_ok = False
+    assert grammar_ok == (text in _JSON_BUT_NOT_FACTORPAIRS)
     with pytest.raises(ValueError, match="offset %d$" % where):
         ctx.exchange_decode(text, 2)
+
+
+@pytest.mark.parametrize("text,npairs,where", [
+    (b'[x{"a":1,"b":2}]', 1, 7),
+    (b'x[{"a":1,"b":2}]', 1, 0),
+    (b'[{"a":1,"b":2}x]', 1, 12),
+    (b'[ x ]', 0, 2),
+    (b'[,]', 0, 1),
+])
+def test_exchange_decode_rejects_edges(ctx, text, npairs, where):
+    with pytest.raises(ValueError):
+        json.loads(text)
+    with pytest.raises(ValueError, match="offset %d$" % where):
+        ctx.exchange_decode(text, npairs)
+
+
+def test_exchange_decode_block_boundaries(ctx):
+    """Numbers and their keys straddling the 16 KiB workgroup spans, long
+    whitespace runs longer than the staged window, "-0" and zeros."""
+    pairs = _random_pairs(4000, 7)
+    pairs[5] = (0, -0)
+    items = ["{%s\"a\"%s:%s%d%s,%s\"b\":%d}" % (" " * (k % 7), "\n" * (k % 3), " " * (k % 5),
+                                                a, " " * (k % 2), " " * (300 if k % 97 == 0 else 0), b)
+             for k, (a, b) in enumerate(pairs)]
+    text = ("[" + " " * 1000 + ",".join(items) + "\t" * 700 + "]").encode()
+    assert [tuple(d.values()) for d in json.loads(text)] == pairs
+    mag, neg = _diff_arrays(pairs)
+    for off in (0, 1, 5):  # shift every number across the span boundaries
+        m2, n2 = ctx.exchange_decode(b" " * off + text, len(pairs))
+        assert np.array_equal(m2, mag)
+        neg_exp = neg.copy()
+        neg_exp[(mag == 0).all(axis=2)] = 0
+        assert np.array_equal(n2, neg_exp)
 
 
 def test_exchange_decode_count_and_brackets(ctx):
