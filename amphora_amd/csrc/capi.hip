@@ -213,10 +213,9 @@ int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
 //   directly.  Verify failures land in one device word per batch; the
 //   smallest global index is reported.
 template <class Launch>
-int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
-                const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
-                Launch&& launch) {
-  if (!c->sub.empty()) return run_sharded(c, words, ins, outs, with_ff, first_fail, launch);
+int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
+                     const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
+                     Launch& launch) {
   if (first_fail) *first_fail = -1;
   if (words == 0) return AMPH_OK;
   constexpr int S = amph_ctx::kSlots;
@@ -331,6 +330,24 @@ int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
     }
   }
   return AMPH_OK;
+}
+
+// An error part-way through leaves earlier batches' copies in flight (into
+// the caller's page-locked buffers, or the slots): wait for them before
+// returning, so nothing writes caller memory after the call has returned.
+template <class Launch>
+int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
+                const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
+                Launch&& launch) {
+  if (!c->sub.empty()) return run_sharded(c, words, ins, outs, with_ff, first_fail, launch);
+  const int rc = run_batched_impl(c, words, ins, outs, with_ff, first_fail, launch);
+  if (rc != AMPH_OK && rc != AMPH_E_VERIFY) {
+    for (int s = 0; s < amph_ctx::kSlots; ++s) {
+      if (c->streams[s]) (void)hipStreamSynchronize(c->streams[s]);
+      c->slots[s].busy = false;
+    }
+  }
+  return rc;
 }
 
 // Multi-device context: contiguous shards of ceil(words / ndev), one thread
@@ -845,14 +862,16 @@ int run_tail(amph_ctx* c, const void* in, size_t in_bytes, void* out, size_t out
   HIP_TRY(hipSetDevice(c->device));
   hipError_t e = c->tail.ensure(512);
   if (e != hipSuccess) return fail(AMPH_E_NOMEM, "tail scratch");
+  if (!c->streams[0]) HIP_TRY(hipStreamCreateWithFlags(&c->streams[0], hipStreamNonBlocking));
+  hipStream_t s = c->streams[0];  // the context's own stream: no device-wide sync
   uint8_t* d = (uint8_t*)c->tail.p;
-  HIP_TRY(hipMemcpy(d, in, in_bytes, hipMemcpyHostToDevice));
-  if (with_bad) HIP_TRY(hipMemset(d + 448, 0x7F, 8));
-  e = launch(d, d + 256, (unsigned long long*)(d + 448), cfg(c, nullptr, 1));
+  HIP_TRY(hipMemcpyAsync(d, in, in_bytes, hipMemcpyHostToDevice, s));
+  if (with_bad) HIP_TRY(hipMemsetAsync(d + 448, 0x7F, 8, s));
+  e = launch(d, d + 256, (unsigned long long*)(d + 448), cfg(c, s, 1));
   if (e != hipSuccess) return hip_fail(e, "codec tail");
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out, d + 256, out_bytes, hipMemcpyDeviceToHost));
-  if (with_bad) HIP_TRY(hipMemcpy(bad_host, d + 448, 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpyAsync(out, d + 256, out_bytes, hipMemcpyDeviceToHost, s));
+  if (with_bad) HIP_TRY(hipMemcpyAsync(bad_host, d + 448, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
   return AMPH_OK;
 }
 }  // namespace
