@@ -220,25 +220,39 @@ class Context:
             arr[j] = _AmphOdo(*[_ptr(f) for f in fs], nbytes)
         return arr, views
 
+    def _out(self, like, shape, out):
+        """A fresh output buffer, or the caller's `out` (same memory kind,
+        C-contiguous uint8 of exactly `shape`) so repeated calls reuse one
+        (page-locked, if the caller registered it) buffer."""
+        if out is None:
+            return self._empty(like, shape)
+        if _is_dev(out) != _is_dev(like):
+            raise ValueError("out must live where the inputs live")
+        ok = (tuple(out.shape) == tuple(shape) and str(out.dtype).endswith("uint8") and
+              (out.is_contiguous() if _is_dev(out) else out.flags["C_CONTIGUOUS"]))
+        if not ok:
+            raise ValueError("out must be a C-contiguous uint8 array of shape %r" % (shape,))
+        return out
+
     # -- client --------------------------------------------------------------
-    def recombine_verify(self, odos):
+    def recombine_verify(self, odos, out=None):
         """odos: list over parties of (y, r, v, w, u) word arrays.
         Returns (canonical secrets (W,16), first_fail) -- first_fail is -1 /
         index on the host path, an int64[1] device tensor on the device path."""
         arr, views = self._odo_structs(odos)
         flags, stream = self._mode(*[f for v in views for f in v])
         W = views[0][0].shape[0]
-        out = self._empty(views[0][0], (W, 16))
+        out = self._out(views[0][0], (W, 16), out)
         ff, ffp = self._ff(views[0][0])
         self._check(lib.amph_recombine_verify(self._h, arr, len(odos), _ptr(out), ffp, flags,
                                               stream), allow_verify=True)
         return out, self._ff_value(ff)
 
-    def mask_input(self, mask_odos, secrets16):
+    def mask_input(self, mask_odos, secrets16, out=None):
         arr, views = self._odo_structs(mask_odos)
         s = words_view(secrets16)
         flags, stream = self._mode(s, *[f for v in views for f in v])
-        out = self._empty(s, (s.shape[0], 16))
+        out = self._out(s, (s.shape[0], 16), out)
         ff, ffp = self._ff(s)
         self._check(lib.amph_mask_input(self._h, arr, len(mask_odos), _ptr(s), s.shape[0],
                                         _ptr(out), ffp, flags, stream), allow_verify=True)

@@ -1,9 +1,10 @@
 // C ABI of libamphora_hip (declared in include/amphora.h).
 //
 // Host-pointer calls stream the word arrays through the device in batches
-// (ctx->batch_words, default 4 Mi words): per batch the inputs go HtoD on one
-// of two HIP streams, the kernel runs, the outputs come back DtoH; two
-// device-side slots let batch k+1's copies overlap batch k's kernel.  Verify
+// (ctx->batch_words, default 4 Mi words): per batch the inputs go HtoD on the
+// copy-in stream, the kernel runs on the kernel stream, the outputs come back
+// DtoH on the copy-out stream; three device-side slots let batch k+1's copies
+// overlap batch k's kernel and batch k-1's copy out (run_batched).  Verify
 // failures are reported per batch into a device array of first-fail words,
 // read back once at the end.  Device-pointer calls (AMPH_F_DEVICE) launch
 // straight onto the caller's stream.
@@ -110,11 +111,12 @@ struct amph_ctx {
   struct Slot {
     DevBuf dev;
     amph::PinnedBuf hin, hout;
-    hipEvent_t done = nullptr;
-    bool busy = false;
+    hipEvent_t in_done = nullptr, k_done = nullptr, out_done = nullptr;
+    bool busy = false;  // hout holds outputs not yet copied to the caller
+    bool used = false;  // the slot has a batch in this call (its events are live)
     size_t base = 0, cnt = 0;
   };
-  hipStream_t streams[kSlots] = {};
+  hipStream_t streams[kSlots] = {};  // host path: HtoD, kernels, DtoH
   Slot slots[kSlots];
   std::vector<amph_ctx*> sub;  // amph_ctx_create_multi: one context per device
   DevBuf ff;  // per-batch first-fail words (host path)
@@ -204,14 +206,22 @@ int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
                 const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
                 Launch& launch);
 
-// Streams `words` through the device in batches of ctx->batch_words:
-//   stage inputs (CPU threads: pageable -> page-locked slot), HtoD, kernel,
-//   DtoH (-> page-locked slot), and copy outputs back once the slot's event
-//   fires.  kSlots batches are in flight on kSlots streams, so the HtoD of
-//   batch b+1, the kernel of batch b and the DtoH of batch b-1 overlap while
-//   the CPU stages the next batch.  Page-locked caller buffers are DMA'd
-//   directly.  Verify failures land in one device word per batch; the
-//   smallest global index is reported.
+// Streams `words` through the device in batches of ctx->batch_words, one
+// HIP stream per engine: streams[0] carries every HtoD copy in batch order,
+// streams[1] the kernels, streams[2] every DtoH copy.  kSlots device slots
+// (inputs + outputs of one batch each) rotate; events order the slot reuse
+// on the GPU (batch b's HtoD waits for the kernel of batch b - kSlots, its
+// kernel for its HtoD and for the DtoH of batch b - kSlots, its DtoH for its
+// kernel), so the copy-in engine streams batch after batch at the link's
+// rate while kernels and copies out overlap it (with one stream per slot the
+// slots' copies shared the link, finished together, and the link idled while
+// their kernels and copies out drained: 2-4 ms every third batch in the
+// rocprofv3 memory-copy trace of a C5 step).  The CPU only
+// waits to reuse a page-locked staging slot: pageable inputs are copied into
+// one by CPU threads once its previous HtoD is done, pageable outputs out of
+// one once its previous DtoH is done.  Page-locked caller buffers are DMA'd
+// directly.  Verify failures land in one device word per batch; the smallest
+// global index is reported.
 template <class Launch>
 int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
                      const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
@@ -219,12 +229,17 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
   if (first_fail) *first_fail = -1;
   if (words == 0) return AMPH_OK;
   constexpr int S = amph_ctx::kSlots;
+  static_assert(S >= 3, "one stream per engine");
   HIP_TRY(hipSetDevice(c->device));
   for (int s = 0; s < S; ++s) {
     if (!c->streams[s]) HIP_TRY(hipStreamCreateWithFlags(&c->streams[s], hipStreamNonBlocking));
-    if (!c->slots[s].done) HIP_TRY(hipEventCreateWithFlags(&c->slots[s].done, hipEventDisableTiming));
-    c->slots[s].busy = false;
+    amph_ctx::Slot& sl = c->slots[s];
+    for (hipEvent_t* e : {&sl.in_done, &sl.k_done, &sl.out_done})
+      if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    sl.busy = false;
+    sl.used = false;
   }
+  hipStream_t s_in = c->streams[0], s_k = c->streams[1], s_out = c->streams[2];
   if (!c->pool) c->pool.reset(new amph::CopyPool(host_threads() - 1));
   const size_t bw = std::min(words, c->batch_words);
   const size_t nb = (words + bw - 1) / bw;
@@ -249,12 +264,12 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
   if (with_ff) {
     hipError_t e = c->ff.ensure(nb * sizeof(unsigned long long));
     if (e != hipSuccess) return fail(AMPH_E_NOMEM, "first-fail words");
-    HIP_TRY(hipMemsetAsync(c->ff.p, 0x7F, nb * sizeof(unsigned long long), c->streams[0]));
-    HIP_TRY(hipStreamSynchronize(c->streams[0]));
+    HIP_TRY(hipMemsetAsync(c->ff.p, 0x7F, nb * sizeof(unsigned long long), s_k));
   }
-  auto drain = [&](amph_ctx::Slot& sl) -> int {
+  // copy a finished batch's pageable outputs from the slot's staging buffer
+  auto drain_out = [&](amph_ctx::Slot& sl) -> int {
     if (!sl.busy) return AMPH_OK;
-    HIP_TRY(hipEventSynchronize(sl.done));
+    HIP_TRY(hipEventSynchronize(sl.out_done));
     std::vector<amph::CopyTask> tasks;
     size_t off = 0;
     for (size_t k = 0; k < outs.size(); ++k) {
@@ -269,10 +284,9 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
   };
   for (size_t b = 0; b < nb; ++b) {
     amph_ctx::Slot& sl = c->slots[b % S];
-    hipStream_t st = c->streams[b % S];
-    if (int rc = drain(sl)) return rc;
     const size_t base = b * bw, cnt = std::min(bw, words - base);
-    // stage pageable inputs into the slot's page-locked buffer
+    // stage pageable inputs into the slot's page-locked buffer once the slot's
+    // previous HtoD has read it
     std::vector<amph::CopyTask> tasks;
     std::vector<const void*> src(ins.size());
     size_t hoff = 0;
@@ -287,22 +301,33 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
         hoff += align256(bw * ins[k].bytes_per_word);
       }
     }
-    c->pool->copy(tasks);
+    if (!tasks.empty()) {
+      if (sl.used) HIP_TRY(hipEventSynchronize(sl.in_done));
+      c->pool->copy(tasks);
+    }
     uint8_t* cur = (uint8_t*)sl.dev.p;
     std::vector<const uint4*> din;
     std::vector<uint4*> dout;
+    if (sl.used) HIP_TRY(hipStreamWaitEvent(s_in, sl.k_done, 0));  // inputs consumed
     for (size_t k = 0; k < ins.size(); ++k) {
-      HIP_TRY(hipMemcpyAsync(cur, src[k], cnt * ins[k].bytes_per_word, hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(cur, src[k], cnt * ins[k].bytes_per_word, hipMemcpyHostToDevice, s_in));
       din.push_back((const uint4*)cur);
       cur += align256(bw * ins[k].bytes_per_word);
     }
+    HIP_TRY(hipEventRecord(sl.in_done, s_in));
     for (size_t k = 0; k < outs.size(); ++k) {
       dout.push_back((uint4*)cur);
       cur += align256(bw * outs[k].bytes_per_word);
     }
+    HIP_TRY(hipStreamWaitEvent(s_k, sl.in_done, 0));
+    if (sl.used) HIP_TRY(hipStreamWaitEvent(s_k, sl.out_done, 0));  // outputs copied out
     unsigned long long* ff = with_ff ? (unsigned long long*)c->ff.p + b : nullptr;
-    hipError_t e = launch(din, dout, cnt, ff, cfg(c, st, cnt));
+    hipError_t e = launch(din, dout, cnt, ff, cfg(c, s_k, cnt));
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
+    HIP_TRY(hipEventRecord(sl.k_done, s_k));
+    // the slot's staging buffer still holds the previous batch's outputs
+    if (int rc = drain_out(sl)) return rc;
+    HIP_TRY(hipStreamWaitEvent(s_out, sl.k_done, 0));
     size_t ooff = 0;
     for (size_t k = 0; k < outs.size(); ++k) {
       void* dst = outs[k].host + base * outs[k].bytes_per_word;
@@ -310,15 +335,17 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
         dst = (char*)sl.hout.p + ooff;
         ooff += align256(bw * outs[k].bytes_per_word);
       }
-      HIP_TRY(hipMemcpyAsync(dst, dout[k], cnt * outs[k].bytes_per_word, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(dst, dout[k], cnt * outs[k].bytes_per_word, hipMemcpyDeviceToHost, s_out));
     }
-    HIP_TRY(hipEventRecord(sl.done, st));
-    sl.busy = true;
+    HIP_TRY(hipEventRecord(sl.out_done, s_out));
+    sl.busy = hout_bytes > 0;  // page-locked outputs need no copy-out (s_out is synced below)
+    sl.used = true;
     sl.base = base;
     sl.cnt = cnt;
   }
   for (size_t b = nb > (size_t)S ? nb - S : 0; b < nb; ++b)
-    if (int rc = drain(c->slots[b % S])) return rc;
+    if (int rc = drain_out(c->slots[b % S])) return rc;
+  HIP_TRY(hipStreamSynchronize(s_out));  // page-locked outputs (no staging slot) landed too
   if (with_ff) {
     std::vector<unsigned long long> h(nb);
     HIP_TRY(hipMemcpy(h.data(), c->ff.p, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -514,7 +541,8 @@ void amph_ctx_destroy(amph_ctx* c) {
       c->slots[s].dev.release();
       c->slots[s].hin.release();
       c->slots[s].hout.release();
-      if (c->slots[s].done) (void)hipEventDestroy(c->slots[s].done);
+      for (hipEvent_t e : {c->slots[s].in_done, c->slots[s].k_done, c->slots[s].out_done})
+        if (e) (void)hipEventDestroy(e);
       if (c->streams[s]) (void)hipStreamDestroy(c->streams[s]);
     }
     c->ff.release();

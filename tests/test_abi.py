@@ -127,3 +127,17 @@ def test_multi_device_context_validation(native):
     assert native.Context(P, R, RINV, devices=[0]).device_count == 1
     with pytest.raises(native.AmphoraNativeError, match="inverse"):
         native.Context(P, R, RINV + 1, devices=[0, 0])
+
+
+def test_out_buffer_validation(native):
+    """out= must be a C-contiguous uint8 buffer of the output's exact shape,
+    in the same memory as the inputs (checked before any device work)."""
+    import numpy as np
+    c = native.Context(P, R, RINV)
+    odo = [(np.zeros((4, 16), np.uint8),) * 5]
+    for bad in (np.zeros((3, 16), np.uint8), np.zeros((4, 16), np.int32),
+                np.zeros((16, 4), np.uint8).T):
+        with pytest.raises(ValueError, match="out must be"):
+            c.recombine_verify(odo, out=bad)
+        with pytest.raises(ValueError, match="out must be"):
+            c.mask_input(odo, np.zeros((4, 16), np.uint8), out=bad)

@@ -180,6 +180,37 @@ def test_host_stream_pinned_and_pageable(ctx, F):
     assert np.array_equal(y1, oy) and np.array_equal(y2, oy) and np.array_equal(m2, om)
 
 
+def test_host_outputs_reused_and_page_locked(ctx, F):
+    """Caller-owned output buffers (out=), page-locked or not, reused across
+    calls: batched DtoH straight into them (no staging copy-out)."""
+    W = 50_003
+    odos, _ = F.synth_odos(seed=15, n=3, W=W)
+    secrets = F.synth_words(seed=16, count=W, mont=False)
+    oy, off = F.recombine_verify(odos)
+    om, omf = F.mask_input(secrets, odos)
+    ys = np.zeros((W, 16), np.uint8)
+    ms = np.zeros((W, 16), np.uint8)
+    ctx.set_batch_words(4096)
+    try:
+        for pinned in (False, True, True):
+            if pinned:
+                ctx.host_register(ys)
+                ctx.host_register(ms)
+            try:
+                y, ff = ctx.recombine_verify(odos, out=ys)
+                m, mf = ctx.mask_input(odos, secrets, out=ms)
+            finally:
+                if pinned:
+                    ctx.host_unregister(ys)
+                    ctx.host_unregister(ms)
+            assert y is ys and m is ms and ff == off == -1 and mf == omf == -1
+            assert np.array_equal(ys, oy) and np.array_equal(ms, om)
+            ys[:] = 0
+            ms[:] = 0
+    finally:
+        ctx.set_batch_words(4 << 20)
+
+
 def test_concurrent_callers(ctx, F):
     """Host-path calls from several threads (ctypes releases the GIL): one
     shared context (calls serialise on its lock) and a second context of its
