@@ -1,5 +1,7 @@
 // K_CONV mapping A/B (tool): word per lane (product) vs two lanes per word
-// (lane 2i: value' = value + [m]; lane 2i+1: mac' = mac + [alpha][m]), fully coalesced.
+// (lane 2i: value' = value + [m]; lane 2i+1: mac' = mac + [alpha][m]), fully
+// coalesced, vs word per lane with the workgroup's input-mask tuples and
+// output shares moved through LDS as coalesced 16-B runs (stage_tuples).
 #include "../../amphora_amd/csrc/kernels.hip"
 #include <algorithm>
 #include <cstdio>
@@ -19,6 +21,29 @@ __global__ __launch_bounds__(1024) void k_conv2(const uint4* masked, const uint4
   else z = use_zero ? x : mod_add(x, m, f);
   st(out + t, z);
 }
+template <int BS>
+__global__ __launch_bounds__(BS) void k_conv3(const uint4* masked, const uint4* tuples, size_t words,
+                                             W4 alpha, int use_zero, uint4* out, Fp f) {
+  __shared__ uint4 buf[3 * BS];
+  const size_t i0 = (size_t)blockIdx.x * BS, i = i0 + threadIdx.x;
+  const size_t nblk = min((size_t)BS, words - i0);
+  stage_tuples<2, BS>(buf, tuples + 2 * i0, nblk);
+  uint4 mr = make_uint4(0, 0, 0, 0);
+  if (i < words) mr = ld(masked + i);
+  __syncthreads();
+  if (i < words) {
+    const W4 m = canon<true>(w4(mr), f);
+    const W4 val = canon<true>(w4(buf[3 * threadIdx.x]), f), mac = canon<true>(w4(buf[3 * threadIdx.x + 1]), f);
+    buf[3 * threadIdx.x] = u4(use_zero ? val : mod_add(val, m, f));
+    buf[3 * threadIdx.x + 1] = u4(mod_add(mac, mont_mul(m, alpha, f), f));
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const size_t q = (size_t)r * BS + threadIdx.x;
+    if (q < 2 * nblk) out[2 * i0 + q] = buf[(q >> 1) * 3 + (q & 1)];
+  }
+}
 }}
 __global__ void k_fill(uint4* b, size_t n, Fp f) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -33,26 +58,32 @@ int main() {
   for (int i = 0; i < 4; ++i) { f.p[i] = p[i]; f.r2[i] = r2[i]; }
   f.n0 = 0x2433ffffu; f.big = 1;
   for (size_t W : {(size_t)1 << 20, (size_t)1 << 24}) {
-    uint4 *m, *t, *o1, *o2;
+    uint4 *m, *t, *o1, *o2, *o3;
     CK(hipMalloc(&m, W * 16)); CK(hipMalloc(&t, 2 * W * 16)); CK(hipMalloc(&o1, 2 * W * 16)); CK(hipMalloc(&o2, 2 * W * 16));
+    CK(hipMalloc(&o3, 2 * W * 16));
     hipLaunchKernelGGL(k_fill, dim3(2048), dim3(256), 0, 0, m, W, f);
     hipLaunchKernelGGL(k_fill, dim3(2048), dim3(256), 0, 0, t, 2 * W, f);
     W4 alpha{{123, 456, 789, 0x1000}};
     LaunchCfg c{0, 0, 1024};
-    std::vector<float> ta, tb;
+    std::vector<float> ta, tb, tc, td;
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    for (int r = 0; r < 23; ++r) for (int v = 0; v < 2; ++v) {
+    for (int r = 0; r < 23; ++r) for (int v = 0; v < 4; ++v) {
       CK(hipEventRecord(e0, 0));
       if (v == 0) launch_convert_share(m, t, W, alpha, 0, o1, f, c);
-      else hipLaunchKernelGGL(k_conv2, dim3((2 * W + 1023) / 1024), dim3(1024), 0, 0, m, t, 2 * W, alpha, 0, o2, f);
+      else if (v == 1) hipLaunchKernelGGL(k_conv2, dim3((2 * W + 1023) / 1024), dim3(1024), 0, 0, m, t, 2 * W, alpha, 0, o2, f);
+      else if (v == 2) hipLaunchKernelGGL(k_conv3<256>, dim3((W + 255) / 256), dim3(256), 0, 0, m, t, W, alpha, 0, o3, f);
+      else hipLaunchKernelGGL(k_conv3<512>, dim3((W + 511) / 512), dim3(512), 0, 0, m, t, W, alpha, 0, o3, f);
       CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-      if (r >= 3) (v ? tb : ta).push_back(ms);
+      if (r >= 3) (v == 0 ? ta : v == 1 ? tb : v == 2 ? tc : td).push_back(ms);
     }
-    std::vector<uint4> a(2 * W), b(2 * W);
+    std::vector<uint4> a(2 * W), b(2 * W), d(2 * W);
     CK(hipMemcpy(a.data(), o1, 2 * W * 16, hipMemcpyDeviceToHost)); CK(hipMemcpy(b.data(), o2, 2 * W * 16, hipMemcpyDeviceToHost));
-    std::sort(ta.begin(), ta.end()); std::sort(tb.begin(), tb.end());
-    printf("W=%zu same=%d prod %.2f us %.1f GB/s | two-lane %.2f us %.1f GB/s\n", W, memcmp(a.data(), b.data(), 2 * W * 16) == 0,
-           ta[10] * 1e3, 80.0 * W / (ta[10] * 1e-3) / 1e9, tb[10] * 1e3, 80.0 * W / (tb[10] * 1e-3) / 1e9);
+    CK(hipMemcpy(d.data(), o3, 2 * W * 16, hipMemcpyDeviceToHost));
+    for (auto* v : {&ta, &tb, &tc, &td}) std::sort(v->begin(), v->end());
+    printf("W=%zu same=%d/%d prod %.2f us %.1f GB/s | two-lane %.2f us %.1f GB/s | lds256 %.2f us %.1f GB/s | lds512 %.2f us %.1f GB/s\n", W,
+           memcmp(a.data(), b.data(), 2 * W * 16) == 0, memcmp(a.data(), d.data(), 2 * W * 16) == 0,
+           ta[10] * 1e3, 80.0 * W / (ta[10] * 1e-3) / 1e9, tb[10] * 1e3, 80.0 * W / (tb[10] * 1e-3) / 1e9,
+           tc[10] * 1e3, 80.0 * W / (tc[10] * 1e-3) / 1e9, td[10] * 1e3, 80.0 * W / (td[10] * 1e-3) / 1e9);
   }
 }
