@@ -469,6 +469,26 @@ int amph_time_next_launch(void* start_event, void* stop_event) {
   return AMPH_OK;
 }
 
+int amph_timing_event_create(void** event) {
+  if (!event) return fail(AMPH_E_PARAM, "null event");
+  hipEvent_t e = nullptr;
+  HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+  *event = (void*)e;
+  return AMPH_OK;
+}
+
+int amph_timing_event_destroy(void* event) {
+  if (event) HIP_TRY(hipEventDestroy((hipEvent_t)event));
+  return AMPH_OK;
+}
+
+int amph_timing_event_elapsed_ms(void* start_event, void* stop_event, float* ms) {
+  if (!start_event || !stop_event || !ms) return fail(AMPH_E_PARAM, "null event or result");
+  HIP_TRY(hipEventSynchronize((hipEvent_t)stop_event));
+  HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)start_event, (hipEvent_t)stop_event));
+  return AMPH_OK;
+}
+
 const char* amph_version(void) { return "amphora_amd 0.1.0 (gfx950)"; }
 
 const char* amph_last_error(void) { return g_last_error.c_str(); }

@@ -139,6 +139,15 @@ int amph_host_unregister(amph_ctx* ctx, void* ptr);
  * own dispatch start / end (hipExtLaunchKernel), so hipEventElapsedTime
  * measures the kernel alone.  Either may be NULL.  Used by bench.py. */
 int amph_time_next_launch(void* start_event, void* stop_event);
+/* Timing-only hipEvent_t for amph_time_next_launch, created with
+ * hipEventDisableSystemFence: recording it does no system-scope release, so
+ * it does not write back and invalidate L2 between the timed kernel and the
+ * next one (a default event did, ~10 us per stamped launch at 1 Mi words).
+ * Not for host synchronisation with the work it follows. */
+int amph_timing_event_create(void** event);
+int amph_timing_event_destroy(void* event);
+/* Milliseconds between two recorded, completed timing events. */
+int amph_timing_event_elapsed_ms(void* start_event, void* stop_event, float* ms);
 
 const char* amph_strerror(int status);
 /* Detail of the last error on the calling thread (empty string if none). */

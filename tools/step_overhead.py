@@ -1,7 +1,9 @@
 """Where does a bench step's time go beyond the two kernels? (tool)
 
 Times 200 steps of K_MASK + K_RV at C2 four ways in one process:
-  events  - amph_time_next_launch events on every launch (bench.py today)
+  events  - amph_time_next_launch events (torch, default flags) on every launch
+  nofence - the same with amph_timing_event_create events (no system fence)
+  *_5th   - events on every 5th step only
   plain   - no events
   graph   - 20 steps captured in one torch.cuda.CUDAGraph, replayed
   kernels - sum of the per-kernel event durations (the floor)
@@ -68,6 +70,28 @@ def run_events(reps):
 
 out["events_us_per_step"] = timed(run_events, STEPS)
 out["kernels_us_per_step"] = sum(e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3]) for e in evs) / STEPS * 1e3
+nf = [[A._lib.TimingEvent() for _ in range(4)] for _ in range(STEPS)]
+
+
+class _H:  # amph_time_next_launch takes the raw hipEvent_t
+    def __init__(self, e):
+        self.cuda_event = e.handle
+
+
+nfh = [[_H(e) for e in q] for q in nf]
+
+
+def run_nofence(reps, every=1):
+    for i in range(reps):
+        step(stream, nfh[i] if i % every == 0 else None)
+
+
+out["nofence_us_per_step"] = timed(run_nofence, STEPS)
+out["nofence_kernels_us_per_step"] = sum(q[0].elapsed_ms(q[1]) + q[2].elapsed_ms(q[3])
+                                         for q in nf) / STEPS * 1e3
+out["events_5th_us_per_step"] = timed(lambda r: [step(stream, evs[i] if i % 5 == 0 else None)
+                                                 for i in range(r)], STEPS)
+out["nofence_5th_us_per_step"] = timed(lambda r: run_nofence(r, 5), STEPS)
 out["plain_us_per_step"] = timed(lambda r: [step(stream) for _ in range(r)], STEPS)
 # launch-only CPU cost (no sync): how long does issuing 200 steps take on the host?
 torch.cuda.synchronize()
