@@ -233,7 +233,14 @@ def cpu_baseline(n: int, budget_s: float):
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+    except OSError:
+        pass
     return {"value": done / el, "unit": "words/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_cpus": os.cpu_count(),
             "sample": "%d words x %d reps (%.1f s): C oracle restating the Java BigInteger "
                       "path (maskInput+verify on %d-party mask ODOs, recombine+verify on "
                       "share ODOs), OpenMP %d threads" % (Ws, done // Ws, el, n, threads)}
