@@ -352,6 +352,83 @@ __device__ __forceinline__ void fold(uint32_t (&v)[4], uint32_t mul, uint32_t ad
   ovf |= carry != 0;
 }
 
+// Fast path for the layout Jackson writes (no whitespace):
+//   member 0 (not the first pair):  <digit> '}' ',' '{' '"' k '"' ':' NUM ','
+//   member 1:                <digit> ',' '"' k '"' ':' NUM '}'
+// with every byte read from the LDS window as whole dwords (independent
+// ds_read_b32 + v_alignbyte, no byte-by-byte walk): the digit run is found
+// with SWAR over 44 bytes, then the 40 bytes ENDING at the last digit are
+// read again, the bytes before the first digit forced to '0', and the value
+// assembled as ten 4-digit groups -> five 8-digit groups -> four base-10^8
+// folds.  Returns false for anything else (whitespace, the first or last pair,
+// a leading zero, more than 39 digits, an overflow, a malformed neighbour):
+// the general path then parses the number and reports any error, so both
+// paths accept exactly the same texts.  o = the start's offset in the window
+// (>= kWinPad, so every read below stays inside it).
+struct FastNum {
+  uint32_t v[4];
+  uint32_t dend;   // window offset one past the last digit
+  uint32_t key;    // 'a' / 'b'
+  bool minus;
+};
+
+__device__ __forceinline__ uint32_t lds_dword(const uint32_t* l32, uint32_t o) {
+  return __builtin_amdgcn_alignbyte(l32[(o >> 2) + 1], l32[o >> 2], o & 3u);
+}
+
+__device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, bool member0,
+                                            FastNum& r) {
+  const uint32_t pre0 = lds_dword(l32, o - 8), pre1 = lds_dword(l32, o - 4);
+  // bytes o-4 .. o-1 = '"' k '"' ':'
+  r.key = (pre1 >> 8) & 0xFFu;
+  bool ok = (pre1 & 0xFFFF00FFu) == 0x3A220022u && (r.key == 'a' || r.key == 'b');
+  if (member0)  // bytes o-8 .. o-5 = <digit> '}' ',' '{'
+    ok = ok && (pre0 & 0xFFFFFF00u) == 0x7B2C7D00u && is_digit(pre0 & 0xFFu);
+  else  // bytes o-6 .. o-5 = <digit> ',' (member 0's digits end right at the ',')
+    ok = ok && (pre0 >> 24) == (uint32_t)',' && is_digit((pre0 >> 16) & 0xFFu);
+  const uint32_t first = lds_dword(l32, o);
+  r.minus = (first & 0xFFu) == (uint32_t)'-';
+  const uint32_t ds = o + (r.minus ? 1u : 0u);
+  uint32_t d[11];
+#pragma unroll
+  for (int j = 0; j < 11; ++j) d[j] = lds_dword(l32, ds + 4 * j);
+  uint32_t nd = 44;
+#pragma unroll
+  for (int j = 10; j >= 0; --j) {
+    const uint32_t nondig = ~swar_digit(d[j]) & 0x80808080u;
+    if (nondig) nd = 4 * j + (__builtin_ctz(nondig) >> 3);
+  }
+  ok = ok && nd >= 1 && nd <= 39 && !((d[0] & 0xFFu) == (uint32_t)'0' && nd > 1);
+  if (!ok) return false;
+  r.dend = ds + nd;
+  const uint32_t after = lds_dword(l32, r.dend) & 0xFFu;
+  if (after != (member0 ? (uint32_t)',' : (uint32_t)'}')) return false;
+  // the 40 bytes ending at the last digit; s = 40 - nd leading bytes -> '0'
+  const uint32_t base = r.dend - 40, s = 40 - nd;
+  uint32_t h[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    uint32_t g[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int j = 2 * k + q;
+      const uint32_t e = lds_dword(l32, base + 4 * j);
+      const int drop = min(max((int)s - 4 * j, 0), 4);
+      const uint32_t keep = drop >= 4 ? 0u : (0xFFFFFFFFu << (8 * drop));
+      const uint32_t v = ((e & keep) | (0x30303030u & ~keep)) - 0x30303030u;
+      const uint32_t t = v * 10u + (v >> 8);
+      g[q] = (t & 0xFFu) * 100u + ((t >> 16) & 0xFFu);
+    }
+    h[k] = g[0] * 10000u + g[1];
+  }
+  r.v[0] = h[0];
+  r.v[1] = r.v[2] = r.v[3] = 0;
+  bool ovf = false;
+#pragma unroll
+  for (int k = 1; k < 5; ++k) fold(r.v, 100000000u, h[k], ovf);
+  return !ovf;
+}
+
 // Pass 3: each workgroup finds its number starts again (from LDS), scans
 // them to global number indices and lists their positions in LDS; then its
 // lanes take ONE NUMBER EACH, consecutive numbers on consecutive lanes (so a
@@ -397,10 +474,24 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint6
   const uint32_t nloc = (uint32_t)min(total, (uint64_t)kMaxStarts);
   const uint64_t gbase = bscan[blockIdx.x];
   // phase 1: own checks + value
+  const uint32_t* l32 = reinterpret_cast<const uint32_t*>(win4);
   for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
     const size_t x = b0 + pos[idx];
     const uint64_t g = gbase + idx;
     const bool first_m = (g & 1) == 0;
+    if (g > 0 && g + 1 < nvals) {
+      FastNum fn;
+      const uint32_t o = (uint32_t)(x - (size_t)w0);
+      if (fast_number(l32, o, first_m, fn)) {
+        endp[idx] = (uint16_t)fn.dend;
+        comma[idx] = (uint16_t)(o - 5);  // member 1: one past the byte before its ','
+        keyc[idx] = (uint8_t)fn.key;
+        const size_t slot = (g & ~(uint64_t)1) + (fn.key == 'b');
+        mag[slot] = make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]);
+        neg[slot] = fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0;
+        continue;
+      }
+    }
     size_t q = 0;
     const uint32_t key = key_before(t, x, &q);
     bool ok = key != 0 && g < nvals && q > 0;
