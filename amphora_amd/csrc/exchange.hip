@@ -256,14 +256,28 @@ __device__ __forceinline__ uint32_t swar_digit(uint32_t w) {
   const uint32_t lo = w & 0x7F7F7F7Fu;
   return (lo + 0x50505050u) & ~(lo + 0x46464646u) & ~w & 0x80808080u;  // 0x30 <= b <= 0x39
 }
-__device__ __forceinline__ uint32_t swar_eq(uint32_t w, uint32_t ch) {
-  const uint32_t y = w ^ (ch * 0x01010101u);
-  return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
+// Number-token byte classes of 4 text bytes by table lookup (v_perm_b32 as an
+// 8-entry byte table): class = HI[b >> 4] & LO[b & 15] with the bits
+//   1 '+' '-' '.' (high nibble 2, low nibble B / D / E)   2 '-' (start)
+//   4 digits (high nibble 3, low nibble 0-9)              8 'e' 'E' (high 6 / 4, low 5)
+// num: bit 7 of byte j set iff byte j continues a number token (digits, sign,
+// fraction, exponent); start: iff it may start one (digit or '-').  Bytes
+// >= 0x80 are in neither class.  19 VALU ops for both masks (bitwise compares
+// took ~40).
+__device__ __forceinline__ void num_classes(uint32_t w, uint32_t& num, uint32_t& start) {
+  const uint32_t lo = w & 0x0F0F0F0Fu, l7 = lo & 0x07070707u;
+  const uint32_t la = __builtin_amdgcn_perm(0x04040C04u, 0x04040404u, l7);  // LO[0..7]
+  const uint32_t lb = __builtin_amdgcn_perm(0x00010300u, 0x01000404u, l7);  // LO[8..15]
+  const uint32_t cl = __builtin_amdgcn_perm(lb, la, 0x03020100u | ((lo & 0x08080808u) >> 1));
+  const uint32_t ch = __builtin_amdgcn_perm(0x00080008u, 0x04030000u, (w >> 4) & 0x07070707u);
+  const uint32_t cls = ch & cl, ascii = ~w & 0x80808080u;
+  num = (cls + 0x7F7F7F7Fu) & ascii;
+  start = ((cls & 0x06060606u) + 0x7F7F7F7Fu) & ascii;
 }
-// bytes that continue a JSON number token (digits, sign, fraction, exponent)
 __device__ __forceinline__ uint32_t swar_numchar(uint32_t w) {
-  return swar_digit(w) | swar_eq(w, '-') | swar_eq(w, '+') | swar_eq(w, '.') | swar_eq(w, 'e') |
-         swar_eq(w, 'E');
+  uint32_t num, start;
+  num_classes(w, num, start);
+  return num;
 }
 
 // Number starts in 32 text bytes (8 dwords): a digit or '-' whose predecessor
@@ -273,9 +287,10 @@ __device__ __forceinline__ uint32_t starts32(const uint32_t (&w)[8], uint32_t pr
   uint32_t m = 0;
 #pragma unroll
   for (int d = 0; d < 8; ++d) {
-    const uint32_t nc = swar_numchar(w[d]);
+    uint32_t nc, st;
+    num_classes(w[d], nc, st);
     const uint32_t pnc = (nc << 8) | (prev_nc >> 24);
-    const uint32_t s = ((swar_digit(w[d]) | swar_eq(w[d], '-')) & ~pnc & 0x80808080u) >> 7;
+    const uint32_t s = (st & ~pnc) >> 7;
     m |= ((s | (s >> 7) | (s >> 14) | (s >> 21)) & 0xFu) << (4 * d);
     prev_nc = nc;
   }
@@ -352,16 +367,33 @@ __device__ __forceinline__ void fold(uint32_t (&v)[4], uint32_t mul, uint32_t ad
   ovf |= carry != 0;
 }
 
+// 8 ASCII digits (little-endian bytes, first digit lowest) -> value < 10^8
+__device__ __forceinline__ uint32_t digits4(uint32_t w) {
+  const uint32_t v = w - 0x30303030u;
+  const uint32_t t = v * 10u + (v >> 8);
+  return (t & 0xFFu) * 100u + ((t >> 16) & 0xFFu);
+}
+__device__ __forceinline__ uint32_t digits8(uint32_t lo, uint32_t hi) {
+  return digits4(lo) * 10000u + digits4(hi);
+}
+__device__ __forceinline__ uint32_t pow10_small(uint32_t k) {  // k <= 8
+  uint32_t p = 1;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i)
+    if (i < k) p *= 10u;
+  return p;
+}
+
 // Fast path for the layout Jackson writes (no whitespace):
 //   member 0 (not the first pair):  <digit> '}' ',' '{' '"' k '"' ':' NUM ','
 //   member 1:                <digit> ',' '"' k '"' ':' NUM '}'
 // with every byte read from the LDS window as whole dwords (independent
 // ds_read_b32 + v_alignbyte, no byte-by-byte walk): the digit run is found
-// with SWAR over 44 bytes, then the 40 bytes ENDING at the last digit are
-// read again, the bytes before the first digit forced to '0', and the value
-// assembled as ten 4-digit groups -> five 8-digit groups -> four base-10^8
-// folds.  Returns false for anything else (whitespace, the first or last pair,
-// a leading zero, more than 39 digits, an overflow, a malformed neighbour):
+// with SWAR over 44 bytes held in registers, and the value is folded in
+// base 10^8 from the same registers: full 8-digit chunks, then the partial
+// last chunk right-aligned behind '0's.  Returns false for anything else
+// (whitespace, the first or last pair, a leading zero, more than 39 digits,
+// an overflow, a malformed neighbour):
 // the general path then parses the number and reports any error, so both
 // paths accept exactly the same texts.  o = the start's offset in the window
 // (>= kWinPad, so every read below stays inside it).
@@ -403,29 +435,24 @@ __device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, boo
   r.dend = ds + nd;
   const uint32_t after = lds_dword(l32, r.dend) & 0xFFu;
   if (after != (member0 ? (uint32_t)',' : (uint32_t)'}')) return false;
-  // the 40 bytes ending at the last digit; s = 40 - nd leading bytes -> '0'
-  const uint32_t base = r.dend - 40, s = 40 - nd;
-  uint32_t h[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    uint32_t g[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int j = 2 * k + q;
-      const uint32_t e = lds_dword(l32, base + 4 * j);
-      const int drop = min(max((int)s - 4 * j, 0), 4);
-      const uint32_t keep = drop >= 4 ? 0u : (0xFFFFFFFFu << (8 * drop));
-      const uint32_t v = ((e & keep) | (0x30303030u & ~keep)) - 0x30303030u;
-      const uint32_t t = v * 10u + (v >> 8);
-      g[q] = (t & 0xFFu) * 100u + ((t >> 16) & 0xFFu);
-    }
-    h[k] = g[0] * 10000u + g[1];
-  }
-  r.v[0] = h[0];
-  r.v[1] = r.v[2] = r.v[3] = 0;
+  // full 8-digit chunks straight from the registers, then the rem = nd % 8
+  // leading digits of the next chunk right-aligned behind '0's
+  const uint32_t full = nd >> 3, rem = nd & 7u;
+  r.v[0] = r.v[1] = r.v[2] = r.v[3] = 0;
   bool ovf = false;
 #pragma unroll
-  for (int k = 1; k < 5; ++k) fold(r.v, 100000000u, h[k], ovf);
+  for (uint32_t m = 0; m < 5; ++m)
+    if (m < full) fold(r.v, 100000000u, digits8(d[2 * m], d[2 * m + 1]), ovf);
+  if (rem) {
+    uint32_t lo = d[0], hi = d[1];
+#pragma unroll
+    for (uint32_t m = 1; m < 5; ++m)
+      if (m == full) { lo = d[2 * m]; hi = d[2 * m + 1]; }
+    const uint64_t x = ((uint64_t)hi << 32) | lo;
+    const uint32_t sh = 8 * (8 - rem);  // 8..56
+    const uint64_t y = (x << sh) | (0x3030303030303030ull >> (64 - sh));
+    fold(r.v, pow10_small(rem), digits8((uint32_t)y, (uint32_t)(y >> 32)), ovf);
+  }
   return !ovf;
 }
 
