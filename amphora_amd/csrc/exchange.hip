@@ -35,6 +35,8 @@ namespace amph {
 
 namespace {
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 constexpr int kXBlock = 256;      // pairs per workgroup (encode)
 constexpr int kXEntry = 92;       // max entry: {"a":-<39 digits>,"b":-<39 digits>},
 constexpr int kScanBlock = 1024;  // elements per workgroup of the scan passes
@@ -302,18 +304,44 @@ constexpr size_t kDecSpan = (size_t)kDecBlock * kDecBytes;  // 16 KiB of text pe
 constexpr int kWinPad = 256;                           // window context either side
 constexpr int kWin = (int)kDecSpan + 2 * kWinPad;      // staged bytes
 
-// Pass 1: number starts per workgroup.
-__global__ __launch_bounds__(kDecBlock) void k_xdec_count(Text t, uint64_t* bsum) {
-  const size_t base = (size_t)blockIdx.x * kDecSpan + (size_t)threadIdx.x * kDecBytes;
-  const uint4 c0 = t.chunk((long long)base), c1 = t.chunk((long long)base + 16);
-  const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+// Pass 1: number starts per 16 KiB span.  256 lanes x 64 bytes (four 16-B
+// loads in flight per lane, nontemporal: the text is read once here and once
+// by the parse), a wave reduction and one LDS word per wave.
+constexpr int kCntBlock = 256;
+constexpr int kCntBytes = (int)(kDecSpan / kCntBlock);  // 64
+static_assert(kCntBytes == 64, "count lanes read four 16-B chunks");
+
+__global__ __launch_bounds__(kCntBlock) void k_xdec_count(Text t, uint64_t* bsum) {
+  __shared__ uint32_t wsum[kCntBlock / 64];
+  const size_t base = (size_t)blockIdx.x * kDecSpan + (size_t)threadIdx.x * kCntBytes;
+  uint4 c[4];
+  if (base >= t.mis && base + kCntBytes <= t.L) {
+    const u32x4* p = reinterpret_cast<const u32x4*>(t.al + base);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const u32x4 v = __builtin_nontemporal_load(p + k);
+      c[k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = t.chunk((long long)base + 16 * k);
+  }
+  const uint32_t w0[8] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w};
+  const uint32_t w1[8] = {c[2].x, c[2].y, c[2].z, c[2].w, c[3].x, c[3].y, c[3].z, c[3].w};
   // numchar flag of the byte before: the previous lane's last dword (lane 0: a load)
-  const uint32_t prev_last = __shfl_up(w[7], 1, 64);
+  const uint32_t prev_last = __shfl_up(w1[7], 1, 64);
   const uint32_t pb = __lane_id() == 0 ? (base ? t[base - 1] : (uint32_t)' ') << 24 : prev_last;
-  const uint64_t cnt = __popc(starts32(w, swar_numchar(pb)));
-  uint64_t total;
-  block_excl_scan(cnt, &total);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+  uint32_t cnt = __popc(starts32(w0, swar_numchar(pb))) + __popc(starts32(w1, swar_numchar(w0[7])));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  if (__lane_id() == 0) wsum[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t total = 0;
+#pragma unroll
+    for (int k = 0; k < kCntBlock / 64; ++k) total += wsum[k];
+    bsum[blockIdx.x] = total;
+  }
 }
 
 // The workgroup's 16 KiB plus kWinPad bytes either side, staged in LDS;
@@ -695,7 +723,7 @@ hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, u
   c0.ev_stop = nullptr;
   cm.ev_start = cm.ev_stop = nullptr;
   c1.ev_start = nullptr;
-  AMPH_LAUNCH(k_xdec_count, dim3((unsigned)nb), dim3(kDecBlock), c0, t, bscan);
+  AMPH_LAUNCH(k_xdec_count, dim3((unsigned)nb), dim3(kCntBlock), c0, t, bscan);
   hipError_t e = scan_u64(bscan, nb, bsum, cm);
   if (e != hipSuccess) return e;
   AMPH_LAUNCH(k_xdec_parse, dim3((unsigned)nb), dim3(kDecBlock), cm, t, bscan, 2 * npairs, mag, neg, bad);
