@@ -37,6 +37,34 @@ __device__ __forceinline__ uint32_t dec6(uint32_t c) {
   return v;
 }
 
+// 4 base64 chars (little-endian bytes, first char lowest) -> the 24-bit group
+// (first char in the top 6 bits).  inv: bit 7 of byte j set iff char j is
+// not in the alphabet.  Table lookups with v_perm_b32 (8-entry byte tables):
+// class = HI[c >> 4] & LO[c & 15], valid iff nonzero, with the bits
+//   1 '+' '/' (high nibble 2, low B / F)   2 digits (high 3, low 0-9)
+//   4 'A'-'O' 'a'-'o' (high 4 / 6, low 1-15)   8 'P'-'Z' 'p'-'z' (high 5 / 7, low 0-A)
+//   0x10 '/' (low F within high 2);
+// value = c + ROLL[c >> 4] bytewise (carry-free), 3 less for '/'.  ~27 VALU
+// ops per 4 chars (dec6's compare/select chain took ~17 per char).
+__device__ __forceinline__ uint32_t dec4(uint32_t w, uint32_t& inv) {
+  const uint32_t lo = w & 0x0F0F0F0Fu, l7 = lo & 0x07070707u, h7 = (w >> 4) & 0x07070707u;
+  const uint32_t la = __builtin_amdgcn_perm(0x0E0E0E0Eu, 0x0E0E0E0Au, l7);  // LO[0..7]
+  const uint32_t lb = __builtin_amdgcn_perm(0x15040404u, 0x050C0E0Eu, l7);  // LO[8..15]
+  const uint32_t cl = __builtin_amdgcn_perm(lb, la, 0x03020100u | ((lo & 0x08080808u) >> 1));
+  const uint32_t cls = __builtin_amdgcn_perm(0x08040804u, 0x02110000u, h7) & cl;
+  inv = ~(((cls & 0x0F0F0F0Fu) + 0x7F7F7F7Fu) & ~w) & 0x80808080u;
+  const uint32_t roll = __builtin_amdgcn_perm(0xB9B9BFBFu, 0x04130000u, h7);
+  uint32_t v = ((w & 0x7F7F7F7Fu) + (roll & 0x7F7F7F7Fu)) ^ ((w ^ roll) & 0x80808080u);
+  const uint32_t fix = (cls >> 4) & 0x01010101u;
+  v -= fix + (fix << 1);
+  return ((v & 0x3Fu) << 18) | ((v & 0x3F00u) << 4) | ((v >> 10) & 0xFC0u) | (v >> 24);
+}
+
+// group -> its 3 bytes in text order in the low 24 bits
+__device__ __forceinline__ uint32_t group_bytes(uint32_t g) {
+  return __builtin_amdgcn_perm(g, g, 0x0C000102u);
+}
+
 // 3 bytes (big-endian group) -> 4 chars packed little-endian in a uint32
 __device__ __forceinline__ uint32_t enc_group(uint32_t b0, uint32_t b1, uint32_t b2) {
   const uint32_t g = (b0 << 16) | (b1 << 8) | b2;
@@ -168,27 +196,22 @@ __global__ __launch_bounds__(kMaxBlock) void k_b64_unwords(const char* in, size_
     const uint2* p = reinterpret_cast<const uint2*>(in + 24 * i);
     const uint2 x0 = p[0], x1 = p[1], x2 = p[2];
     const uint32_t w[6] = {x0.x, x0.y, x1.x, x1.y, x2.x, x2.y};
-    uint8_t b[18];
-    bool ok = ((w[5] >> 16) & 0xFF) == '=' && (w[5] >> 24) == '=';
+    bool ok = (w[5] >> 16) == 0x3D3Du;  // "=="
+    uint32_t u[6], inv = 0;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
-      uint32_t v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t ch = (w[q] >> (8 * k)) & 0xFF;
-        v[k] = (q == 5 && k >= 2) ? 0u : dec6(ch);
-        ok &= v[k] != 0xFFu;
-      }
-      const uint32_t g = (v[0] << 18) | (v[1] << 12) | (v[2] << 6) | v[3];
-      b[3 * q] = (g >> 16) & 0xFF;
-      b[3 * q + 1] = (g >> 8) & 0xFF;
-      b[3 * q + 2] = g & 0xFF;
+      uint32_t iq;
+      // the last group's two '=' decode as 'A' (value 0); like java.util.Base64
+      // / Jackson, the unused low bits of the last group are ignored
+      u[q] = group_bytes(dec4(q == 5 ? (w[5] & 0xFFFFu) | 0x41410000u : w[q], iq));
+      inv |= iq;
     }
-    // like java.util.Base64 / Jackson, the unused low bits of the last group are ignored
+    ok &= inv == 0;
     uint32_t o[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      o[q] = b[4 * q] | (b[4 * q + 1] << 8) | (b[4 * q + 2] << 16) | ((uint32_t)b[4 * q + 3] << 24);
+    o[0] = u[0] | (u[1] << 24);
+    o[1] = (u[1] >> 8) | (u[2] << 16);
+    o[2] = (u[2] >> 16) | (u[3] << 8);
+    o[3] = u[4] | (u[5] << 24);
     out[i] = make_uint4(o[0], o[1], o[2], o[3]);
     if (!ok) atomicMin(bad, (unsigned long long)(ibase + i));
   }
@@ -237,26 +260,17 @@ __global__ __launch_bounds__(kB64Block) void k_b64_decode_blk(const char* in, ui
   const size_t u0 = (size_t)blockIdx.x * kB64Block, t = u0 + threadIdx.x;
   const uint4 v = ldnt4(reinterpret_cast<const uint4*>(in) + t);
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint32_t firstbad = 0xFFFFFFFFu;
-  uint8_t o[12];
+  uint32_t firstbad = 0xFFFFFFFFu, u[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    uint32_t d[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      d[k] = dec6((w[q] >> (8 * k)) & 0xFF);  // no '=' before the final unit
-      if (d[k] == 0xFFu && firstbad == 0xFFFFFFFFu) firstbad = 4 * q + k;
-    }
-    const uint32_t g = (d[0] << 18) | (d[1] << 12) | (d[2] << 6) | d[3];
-    o[3 * q] = (g >> 16) & 0xFF;
-    o[3 * q + 1] = (g >> 8) & 0xFF;
-    o[3 * q + 2] = g & 0xFF;
+  for (int q = 3; q >= 0; --q) {  // no '=' before the final unit
+    uint32_t inv;
+    u[q] = group_bytes(dec4(w[q], inv));
+    if (inv) firstbad = 4 * q + (__builtin_ctz(inv) >> 3);
   }
   if (firstbad != 0xFFFFFFFFu) atomicMin(bad, (unsigned long long)(16 * t + firstbad));
-#pragma unroll
-  for (int q = 0; q < 3; ++q)
-    lds[3 * threadIdx.x + q] =
-        o[4 * q] | (o[4 * q + 1] << 8) | (o[4 * q + 2] << 16) | ((uint32_t)o[4 * q + 3] << 24);
+  lds[3 * threadIdx.x] = u[0] | (u[1] << 24);
+  lds[3 * threadIdx.x + 1] = (u[1] >> 8) | (u[2] << 16);
+  lds[3 * threadIdx.x + 2] = (u[2] >> 16) | (u[3] << 8);
   __syncthreads();
   uint4* dst = reinterpret_cast<uint4*>(out + 12 * u0);
   for (int q = threadIdx.x; q < 3 * kB64Block / 4; q += kB64Block)

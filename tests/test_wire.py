@@ -135,6 +135,49 @@ def test_base64_words(ctx):
         ctx.base64_decode_words(bad)
 
 
+_B64_ALPHABET = set(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/")
+
+
+def test_base64_block_path_every_byte_value(ctx):
+    """The workgroup-staged stream decoder (full 4096-char blocks) on every
+    byte value at an interior position: alphabet bytes decode like Python's
+    base64, anything else is reported at its index; with two bad bytes the
+    first one is reported."""
+    raw = np.random.default_rng(11).integers(0, 256, 3 * 4096 * 3, dtype=np.uint8).tobytes()
+    enc = base64.b64encode(raw)
+    assert len(enc) % 4096 == 0
+    for b in range(256):
+        pos = 4096 + 13 * b + (b % 4)
+        t = bytearray(enc)
+        t[pos] = b
+        if b in _B64_ALPHABET:
+            assert ctx.base64_decode(bytes(t)) == base64.b64decode(bytes(t))
+        else:
+            with pytest.raises(ValueError, match="index %d$" % pos):
+                ctx.base64_decode(bytes(t))
+    t = bytearray(enc)
+    t[9001] = ord("-")
+    t[5003] = ord("_")
+    with pytest.raises(ValueError, match="index 5003$"):
+        ctx.base64_decode(bytes(t))
+
+
+def test_base64_words_every_byte_value(ctx):
+    """Per-word records: every byte value in every data position of a record."""
+    words = np.random.default_rng(12).integers(0, 256, (4096, 16), dtype=np.uint8)
+    rec = ctx.base64_encode_words(words)
+    for b in range(256):
+        bad = rec.copy()
+        k = 1000 + b
+        bad[k, b % 22] = b
+        if b in _B64_ALPHABET:
+            got = ctx.base64_decode_words(bad)
+            assert got[k].tobytes() == base64.b64decode(bad[k].tobytes())
+        else:
+            with pytest.raises(ValueError, match=str(k)):
+                ctx.base64_decode_words(bad)
+
+
 def test_masked_input_json_roundtrip(ctx):
     import amphora_amd as A
     from amphora_amd import wire
