@@ -22,9 +22,6 @@ namespace amph {
 
 namespace {
 
-__device__ __forceinline__ uint32_t enc6(uint32_t v) {  // 0..63 -> ASCII
-  return v + 65u + 6u * (v >= 26u) - 75u * (v >= 52u) - 15u * (v >= 62u) + 3u * (v >= 63u);
-}
 
 // ASCII -> 0..63, or 0xFF if not in the alphabet
 __device__ __forceinline__ uint32_t dec6(uint32_t c) {
@@ -65,11 +62,22 @@ __device__ __forceinline__ uint32_t group_bytes(uint32_t g) {
   return __builtin_amdgcn_perm(g, g, 0x0C000102u);
 }
 
+// 24-bit group (first char in the top 6 bits) -> its 4 chars, packed
+// little-endian.  SWAR over the four 6-bit values: idx = (v >= 26) + (v >= 52)
+// + (v >= 62) + (v >= 63) picks the offset to ASCII from a v_perm byte table
+// ('A', 'a' - 26, '0' - 52, '+' - 62, '/' - 63), added carry-free.
+__device__ __forceinline__ uint32_t enc4(uint32_t g) {
+  const uint32_t v = ((g >> 18) & 0x3Fu) | ((g >> 4) & 0x3F00u) | ((g << 10) & 0x3F0000u) |
+                     ((g << 24) & 0x3F000000u);
+  const uint32_t idx = (((v + 0x66666666u) >> 7) & 0x01010101u) + (((v + 0x4C4C4C4Cu) >> 7) & 0x01010101u) +
+                       (((v + 0x42424242u) >> 7) & 0x01010101u) + (((v + 0x41414141u) >> 7) & 0x01010101u);
+  const uint32_t off = __builtin_amdgcn_perm(0x000000F0u, 0xEDFC4741u, idx);
+  return ((v & 0x7F7F7F7Fu) + (off & 0x7F7F7F7Fu)) ^ ((v ^ off) & 0x80808080u);
+}
+
 // 3 bytes (big-endian group) -> 4 chars packed little-endian in a uint32
 __device__ __forceinline__ uint32_t enc_group(uint32_t b0, uint32_t b1, uint32_t b2) {
-  const uint32_t g = (b0 << 16) | (b1 << 8) | b2;
-  return enc6((g >> 18) & 63u) | (enc6((g >> 12) & 63u) << 8) | (enc6((g >> 6) & 63u) << 16) |
-         (enc6(g & 63u) << 24);
+  return enc4((b0 << 16) | (b1 << 8) | b2);
 }
 
 __global__ __launch_bounds__(kMaxBlock) void k_b64_encode(const uint8_t* in, size_t nbytes,
