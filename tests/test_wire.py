@@ -297,6 +297,11 @@ def test_exchange_decode_whitespace_and_order(ctx):
     text = json.dumps(items, separators=(" , ", " : ")).encode()
     m3, _ = ctx.exchange_decode(b"  \n" + text + b"\n", 3000)
     assert np.array_equal(m3, mag)
+    # compact (the fast path) with members in either order
+    text = json.dumps(items, separators=(",", ":")).encode()
+    m4, n4 = ctx.exchange_decode(text, 3000)
+    assert np.array_equal(m4, mag)
+    assert np.array_equal(n4, neg)
 
 
 _JSON_BUT_NOT_FACTORPAIRS = {
@@ -339,6 +344,33 @@ def test_exchange_decode_rejects(ctx, text, where):
     assert grammar_ok == (text in _JSON_BUT_NOT_FACTORPAIRS)
     with pytest.raises(ValueError, match="offset %d$" % where):
         ctx.exchange_decode(text, 2)
+
+
+@pytest.mark.parametrize("middle,where", [
+    (b'{"a":1.5,"b":2}', 20), (b'{"a":1e5,"b":2}', 20), (b'{"a":1,"a":2}', 26),
+    (b'{"a":1,"c":2}', 26), (b'{"a":"1","b":2}', 21),
+    (b'{"a":340282366920938463463374607431768211456,"b":2}', 20),
+    (b'{"a":--1,"b":2}', 20), (b'{"a":01,"b":2}', 20), (b'{"a":-00,"b":2}', 20),
+    (b'{"a":1,"b":-}', 26), (b'{"a":1,"b":2 }', 26), (b'{"a": 1,"b":2}', 21),
+])
+def test_exchange_decode_rejects_mid_array(ctx, middle, where):
+    """The same defects in a pair that is neither first nor last, among
+    compact pairs (so the numbers around it take the whitespace-free fast
+    path): the same offset is reported, or none for valid whitespace."""
+    text = b'[{"a":1,"b":2},' + middle + b',{"a":7,"b":8},{"a":-9,"b":10}]'
+    try:
+        items = json.loads(text)
+        valid = all(sorted(d) == ["a", "b"] and all(type(v) is int for v in d.values())
+                    and all(abs(v) < 2 ** 128 for v in d.values()) for d in items)
+    except ValueError:
+        valid = False
+    if valid:
+        mag, neg = ctx.exchange_decode(text, 4)
+        exp_m, exp_n = _diff_arrays([(d["a"], d["b"]) for d in items])
+        assert np.array_equal(mag, exp_m) and np.array_equal(neg, exp_n)
+    else:
+        with pytest.raises(ValueError, match="offset %d$" % where):
+            ctx.exchange_decode(text, 4)
 
 
 @pytest.mark.parametrize("text,npairs,where", [
