@@ -35,6 +35,26 @@ METRIC = "secret words/s device-resident share+recombine, 128-bit prime, 1/2/4/8
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 NO_FAIL = 0x7F7F7F7F7F7F7F7F
 
+# stdout carries exactly ONE line, the JSON result: everything else written to
+# file descriptor 1 (RCCL's version banner, gloo's connection messages, HIP
+# runtime notes) is sent to stderr, and emit() writes to the saved stdout.
+_RESULT_FD = None
+
+
+def _claim_stdout():
+    global _RESULT_FD
+    if _RESULT_FD is None:
+        sys.stdout.flush()
+        _RESULT_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(obj) -> None:
+    data = (json.dumps(obj) + "\n").encode()
+    fd = _RESULT_FD if _RESULT_FD is not None else 1
+    while data:
+        data = data[os.write(fd, data):]
+
 
 def kbytes(kernel: str, n: int) -> int:
     """Algorithmic HBM bytes per word."""
@@ -149,13 +169,12 @@ def scatter_mode(a, A, torch, dist, ctx, rank, world):
     else:
         ok = int(ff.min().item()) == NO_FAIL
     if rank == 0:
-        print(json.dumps({"metric": "secret words/s share+recombine incl. RCCL scatter/gather from one GPU",
-                          "value": W * a.steps / el, "unit": "words/s", "n_gpus": world,
-                          "steps": a.steps, "warmup": a.warmup, "ms_per_step": el * 1e3 / a.steps,
-                          "higher_is_better": True, "scaling": "strong", "verified": ok,
-                          "config": {"workload": "C4: root-held arrays scattered over RCCL",
-                                     "words_total": W, "parties": n,
-                                     "parallelism": "dp%d" % world}}), flush=True)
+        emit({"metric": "secret words/s share+recombine incl. RCCL scatter/gather from one GPU",
+              "value": W * a.steps / el, "unit": "words/s", "n_gpus": world,
+              "steps": a.steps, "warmup": a.warmup, "ms_per_step": el * 1e3 / a.steps,
+              "higher_is_better": True, "scaling": "strong", "verified": ok,
+              "config": {"workload": "C4: root-held arrays scattered over RCCL",
+                         "words_total": W, "parties": n, "parallelism": "dp%d" % world}})
 
 
 def host_mode(a, A, torch, ctx):
@@ -206,7 +225,7 @@ def host_mode(a, A, torch, ctx):
             "verified": ok, "pinned_inputs": a.pin, "batch_words": a.batch_words,
             "host_bytes_per_step": hbytes, "host_GBps": hbytes * a.steps / el / 1e9,
             "config": {"workload": "K_MASK + K_RV from host memory", "words": W, "parties": n}}
-    print(json.dumps(line), flush=True)
+    emit(line)
     if a.pin:
         for arr in (mask_h, share_h, sec_h, masked_h, ys_h):
             ctx.host_unregister(arr)
@@ -248,6 +267,7 @@ def cpu_baseline(n: int, budget_s: float):
 
 def main():
     a = parse()
+    _claim_stdout()
     import torch
     import torch.distributed as dist
     import amphora_amd as A
@@ -389,7 +409,7 @@ def main():
         }
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
-        print(json.dumps(line), flush=True)
+        emit(line)
     if distributed:
         dist.destroy_process_group()
     if not ok:
