@@ -1,6 +1,8 @@
 """Property tests (hypothesis) of the HIP kernels against the C oracle on
 edge-heavy raw words (0, 1, p-1, p, p+1, 2^127, 2^128-1 and uniform 128-bit
 values) and random party counts -- bit-exact, through the C ABI."""
+import os
+
 import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings
@@ -14,8 +16,9 @@ from oracle import coracle  # noqa: E402
 P, R, RINV = O.TEST_PRIME, O.TEST_R, O.TEST_RINV
 EDGE = [0, 1, 2, P - 2, P - 1, P, P + 1, 2 ** 127, 2 ** 128 - 1, 2 ** 128 - P - 1]
 raw_word = st.one_of(st.sampled_from(EDGE), st.integers(0, 2 ** 128 - 1))
-SETTINGS = settings(max_examples=50, deadline=None, suppress_health_check=[HealthCheck.too_slow,
-                                                                           HealthCheck.function_scoped_fixture])
+# AMPH_HYPOTHESIS_EXAMPLES raises the example count for soak runs
+SETTINGS = settings(max_examples=int(os.environ.get("AMPH_HYPOTHESIS_EXAMPLES", "50")), deadline=None,
+                    suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 
 
 @pytest.fixture(scope="module")

@@ -3,6 +3,8 @@ tests use at large sizes -- against the Python restatement of the reference's
 BigInteger code, on edge-heavy raw words: 0, 1, p-1, p, p+1, 2^127, 2^128-1
 (non-canonical words >= p occur in the reference's random-byte fixtures,
 AmphoraTestData.java) and uniform 128-bit values.  CPU only."""
+import os
+
 import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings
@@ -15,7 +17,9 @@ P, R, RINV = O.TEST_PRIME, O.TEST_R, O.TEST_RINV
 SPDZ = O.MpSpdzIntegrationUtils(P, R, RINV)
 EDGE = [0, 1, 2, P - 2, P - 1, P, P + 1, 2 ** 127, 2 ** 128 - 1, 2 ** 128 - P - 1]
 raw_word = st.one_of(st.sampled_from(EDGE), st.integers(0, 2 ** 128 - 1))
-SETTINGS = settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+# AMPH_HYPOTHESIS_EXAMPLES raises the example count for soak runs
+SETTINGS = settings(max_examples=int(os.environ.get("AMPH_HYPOTHESIS_EXAMPLES", "60")), deadline=None,
+                    suppress_health_check=[HealthCheck.too_slow])
 
 
 @pytest.fixture(scope="module")
