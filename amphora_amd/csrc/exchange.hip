@@ -299,6 +299,20 @@ __device__ __forceinline__ uint32_t starts32(const uint32_t (&w)[8], uint32_t pr
   return m;
 }
 
+// The number of starts in 32 text bytes (what __popc(starts32(...)) gives,
+// without packing the per-byte flags into a bit mask).
+__device__ __forceinline__ uint32_t count_starts32(const uint32_t (&w)[8], uint32_t prev_nc) {
+  uint32_t n = 0;
+#pragma unroll
+  for (int d = 0; d < 8; ++d) {
+    uint32_t nc, st;
+    num_classes(w[d], nc, st);
+    n += __popc(st & ~((nc << 8) | (prev_nc >> 24)));
+    prev_nc = nc;
+  }
+  return n;
+}
+
 constexpr int kDecBlock = 512;                         // threads per workgroup
 constexpr size_t kDecSpan = (size_t)kDecBlock * kDecBytes;  // 16 KiB of text per workgroup
 constexpr int kWinPad = 256;                           // window context either side
@@ -331,7 +345,7 @@ __global__ __launch_bounds__(kCntBlock) void k_xdec_count(Text t, uint64_t* bsum
   // numchar flag of the byte before: the previous lane's last dword (lane 0: a load)
   const uint32_t prev_last = __shfl_up(w1[7], 1, 64);
   const uint32_t pb = __lane_id() == 0 ? (base ? t[base - 1] : (uint32_t)' ') << 24 : prev_last;
-  uint32_t cnt = __popc(starts32(w0, swar_numchar(pb))) + __popc(starts32(w1, swar_numchar(w0[7])));
+  uint32_t cnt = count_starts32(w0, swar_numchar(pb)) + count_starts32(w1, swar_numchar(w0[7]));
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
   if (__lane_id() == 0) wsum[threadIdx.x >> 6] = cnt;
