@@ -70,8 +70,10 @@ def config_name(words: int, parties: int) -> str:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=5)
+    # device mode: a C2 step is ~70 us, so 1000 timed steps after 100 warm-up
+    # steps take ~80 ms; host and scatter modes move GBs per step: 5 after 1
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--words", type=int, default=1 << 20, help="words per GPU (C2: 2^20)")
     ap.add_argument("--parties", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -98,7 +100,13 @@ def parse():
     ap.add_argument("--scatter", action="store_true",
                     help="C4: --words is the TOTAL array, held on rank 0 and scattered / "
                          "gathered over RCCL every step (strong scaling)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    bulk = a.mode == "host" or a.scatter
+    if a.steps is None:
+        a.steps = 5 if bulk else 1000
+    if a.warmup is None:
+        a.warmup = 1 if bulk else 100
+    return a
 
 
 def scatter_mode(a, A, torch, dist, ctx, rank, world):
@@ -344,8 +352,8 @@ def main():
     # Sampled kernel timing: `samples` launches of each kernel get timing-only
     # events (no system-scope fence on record), K_MASK and K_RV stamped in
     # different steps spread evenly over the timed region.  A stamped launch
-    # still costs ~3-4 us of dispatch; with the default 200 steps that is
-    # ~0.3 us per step.
+    # still costs ~3-4 us of dispatch; over the default 1000 steps that is
+    # ~0.06 us per step.
     ns = max(1, min(a.samples, a.steps // 2 if a.steps >= 2 else 1))
     mask_at = {int((j + 0.25) * a.steps / ns): j for j in range(ns)}
     rv_at = {int((j + 0.75) * a.steps / ns): j for j in range(ns)}
