@@ -469,7 +469,8 @@ __device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, boo
   uint32_t nd = 44;
 #pragma unroll
   for (int j = 10; j >= 0; --j) {
-    const uint32_t nondig = ~swar_digit(d[j]) & 0x80808080u;
+    const uint32_t x = d[j] ^ 0x30303030u;  // digits -> 0..9
+    const uint32_t nondig = (((x & 0x7F7F7F7Fu) + 0x76767676u) | x) & 0x80808080u;
     if (nondig) nd = 4 * j + (__builtin_ctz(nondig) >> 3);
   }
   ok = ok && nd >= 1 && nd <= 39 && !((d[0] & 0xFFu) == (uint32_t)'0' && nd > 1);
@@ -480,11 +481,21 @@ __device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, boo
   // full 8-digit chunks straight from the registers, then the rem = nd % 8
   // leading digits of the next chunk right-aligned behind '0's
   const uint32_t full = nd >> 3, rem = nd & 7u;
-  r.v[0] = r.v[1] = r.v[2] = r.v[3] = 0;
   bool ovf = false;
+  if (full == 4) {  // 32..39 digits (a random 128-bit value): two 16-digit halves
+    const uint64_t p0 = (uint64_t)digits8(d[0], d[1]) * 100000000u + digits8(d[2], d[3]);
+    const uint64_t p1 = (uint64_t)digits8(d[4], d[5]) * 100000000u + digits8(d[6], d[7]);
+    const unsigned __int128 t = (unsigned __int128)p0 * 10000000000000000ull + p1;  // < 10^32
+    r.v[0] = (uint32_t)t;
+    r.v[1] = (uint32_t)(t >> 32);
+    r.v[2] = (uint32_t)(t >> 64);
+    r.v[3] = (uint32_t)(t >> 96);
+  } else {
+    r.v[0] = r.v[1] = r.v[2] = r.v[3] = 0;
 #pragma unroll
-  for (uint32_t m = 0; m < 5; ++m)
-    if (m < full) fold(r.v, 100000000u, digits8(d[2 * m], d[2 * m + 1]), ovf);
+    for (uint32_t m = 0; m < 4; ++m)
+      if (m < full) fold(r.v, 100000000u, digits8(d[2 * m], d[2 * m + 1]), ovf);
+  }
   if (rem) {
     uint32_t lo = d[0], hi = d[1];
 #pragma unroll
