@@ -398,3 +398,23 @@ def test_baseline_sizes(ctx, F, torch, n, W):
     assert ff_dev(ff) == fault
     del buf
     torch.cuda.empty_cache()
+
+
+def test_timing_events_stamp_the_next_launch(ctx, F, torch):
+    """amph_time_next_launch with amph_timing_event_create events (what
+    bench.py uses): the events time exactly the next kernel launch of an
+    amph_* call, a positive duration far below the wall time of a
+    synchronising call, and the launch's results are unaffected."""
+    import amphora_amd as A
+    W, n = 1 << 20, 2
+    odos, _, _ = ctx.synth_odos(seed=5, n=n, words=W)
+    y0, ff0 = ctx.recombine_verify(odos)
+    torch.cuda.synchronize()
+    e0, e1 = A._lib.TimingEvent(), A._lib.TimingEvent()
+    assert A._lib.lib.amph_time_next_launch(e0.handle, e1.handle) == 0
+    y1, ff1 = ctx.recombine_verify(odos)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_ms(e1)
+    assert 0.0 < ms < 50.0
+    assert int(ff0.item()) == int(ff1.item()) == A._lib.AMPH_NO_FAILURE
+    assert torch.equal(y0, y1)
