@@ -90,20 +90,33 @@ __device__ __forceinline__ char* put_str(char* o, const char* s) {
   return o;
 }
 
+// x < 10^4 -> its 4 ASCII digits, first digit in the lowest byte
+__device__ __forceinline__ uint32_t ascii4(uint32_t x) {
+  const uint32_t a = x / 100u, b = x - 100u * a;
+  const uint32_t a1 = a / 10u, b1 = b / 10u;
+  return 0x30303030u | a1 | ((a - 10u * a1) << 8) | (b1 << 16) | ((b - 10u * b1) << 24);
+}
+
 __device__ __forceinline__ char* put_int(char* o, const uint4& m, bool neg) {
   uint32_t ch[5];
   const int nd = to_chunks(m, ch);
   if (neg && !is_zero(m)) *o++ = '-';  // BigInteger has no negative zero
-  int pos = nd;
-  // digits from the least significant end
+  // chunk k (base 10^9, little end first) holds text positions
+  // [nd - 9 (k + 1), nd - 9 k); its 9 digits come from one division by 10^8,
+  // one by 10^4 and two 4-digit SWAR conversions instead of 9 divisions by 10
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
-    uint32_t x = ch[k];
-    for (int j = 0; j < 9 && pos > 0; ++j) {
-      const uint32_t q = x / 10u;
-      o[--pos] = (char)('0' + (x - 10u * q));
-      x = q;
-    }
+    const int base = nd - 9 * (k + 1);
+    if (base + 9 <= 0) break;
+    const uint32_t c = ch[k], top = c / 100000000u, r = c - top * 100000000u;
+    const uint32_t hi = r / 10000u;
+    const uint32_t w0 = ascii4(hi), w1 = ascii4(r - hi * 10000u);
+    const uint32_t dig[9] = {0x30u + top,      w0 & 0xFFu,         (w0 >> 8) & 0xFFu,
+                             (w0 >> 16) & 0xFFu, w0 >> 24,          w1 & 0xFFu,
+                             (w1 >> 8) & 0xFFu,  (w1 >> 16) & 0xFFu, w1 >> 24};
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+      if (base + j >= 0) o[base + j] = (char)dig[j];
   }
   return o + nd;
 }
