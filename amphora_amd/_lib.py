@@ -78,6 +78,7 @@ def _load():
     L.amph_time_next_launch.argtypes = [vp, vp]
     L.amph_timing_event_create.argtypes = [C.POINTER(vp)]
     L.amph_timing_event_destroy.argtypes = [vp]
+    L.amph_timing_event_record.argtypes = [vp, vp]
     L.amph_timing_event_elapsed_ms.argtypes = [vp, vp, C.POINTER(C.c_float)]
     L.amph_base64_encode.argtypes = [vp, vp, sz, vp, u32, vp]
     L.amph_base64_decode.argtypes = [vp, vp, sz, vp, C.POINTER(C.c_size_t), i64p, u32, vp]
@@ -100,7 +101,7 @@ EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count",
             "amph_mask_words", "amph_to_gfp", "amph_from_gfp", "amph_convert_share",
             "amph_odo_pre", "amph_open_diffs", "amph_odo_post", "amph_synth_odos",
             "amph_synth_words", "amph_host_register", "amph_host_unregister",
-            "amph_time_next_launch", "amph_timing_event_create", "amph_timing_event_destroy",
+            "amph_time_next_launch", "amph_timing_event_create", "amph_timing_event_destroy", "amph_timing_event_record",
             "amph_timing_event_elapsed_ms", "amph_base64_encode", "amph_base64_decode",
             "amph_base64_encode_words", "amph_base64_decode_words", "amph_exchange_max_chars",
             "amph_exchange_encode", "amph_exchange_decode"]

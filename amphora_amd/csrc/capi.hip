@@ -482,6 +482,12 @@ int amph_timing_event_destroy(void* event) {
   return AMPH_OK;
 }
 
+int amph_timing_event_record(void* event, void* stream) {
+  if (!event) return fail(AMPH_E_PARAM, "null event");
+  HIP_TRY(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
+  return AMPH_OK;
+}
+
 int amph_timing_event_elapsed_ms(void* start_event, void* stop_event, float* ms) {
   if (!start_event || !stop_event || !ms) return fail(AMPH_E_PARAM, "null event or result");
   HIP_TRY(hipEventSynchronize((hipEvent_t)stop_event));

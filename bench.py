@@ -81,6 +81,9 @@ def parse():
                     help="event-stamped launches per kernel, spread evenly over the timed "
                          "steps, at most one per step (each costs ~3-4 us of dispatch, "
                          "tools/step_overhead.py)")
+    ap.add_argument("--event-mode", choices=["launch", "record"], default="launch",
+                    help="launch: events stamped by the kernel dispatch (hipExtLaunchKernel); "
+                         "record: hipEventRecord on the stream right before and after the call")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--mode", choices=["device", "host"], default="device",
@@ -335,15 +338,26 @@ def main():
         # kernel timing: hipExtLaunchKernel stamps the events at each kernel's
         # own dispatch start/end (amph_time_next_launch), on the launch stream
         ff0, ff1 = vptr[step_no[0]]
+        rec = a.event_mode == "record"
         if ev_mask is not None:
-            lib.lib.amph_time_next_launch(ev_mask[0].handle, ev_mask[1].handle)
+            if rec:
+                lib.lib.amph_timing_event_record(ev_mask[0].handle, stream)
+            else:
+                lib.lib.amph_time_next_launch(ev_mask[0].handle, ev_mask[1].handle)
         st = lib.lib.amph_mask_input(ctx._h, mask_arr, n, secrets.data_ptr(), W, masked.data_ptr(),
                                      ff0, flags, stream)
         assert st == 0
+        if ev_mask is not None and rec:
+            lib.lib.amph_timing_event_record(ev_mask[1].handle, stream)
         if ev_rv is not None:
-            lib.lib.amph_time_next_launch(ev_rv[0].handle, ev_rv[1].handle)
+            if rec:
+                lib.lib.amph_timing_event_record(ev_rv[0].handle, stream)
+            else:
+                lib.lib.amph_time_next_launch(ev_rv[0].handle, ev_rv[1].handle)
         st = lib.lib.amph_recombine_verify(ctx._h, share_arr, n, ys.data_ptr(), ff1, flags, stream)
         assert st == 0
+        if ev_rv is not None and rec:
+            lib.lib.amph_timing_event_record(ev_rv[1].handle, stream)
         step_no[0] += 1
 
     for _ in range(a.warmup):
@@ -406,9 +420,12 @@ def main():
                        "words_per_gpu": W, "parties": n, "parallelism": "dp%d" % world},
             "verified": ok,
             "kernels_ms": {k: round(v, 5) for k, v in kern.items()},
-            "kernel_timing": "HIP events (hipEventDisableSystemFence) stamped by the kernel "
-                             "dispatch (hipExtLaunchKernel) on the launch stream: %d launches of "
-                             "each kernel spread over the %d timed steps" % (ns, a.steps),
+            "kernel_timing": ("HIP events (hipEventDisableSystemFence) %s on the launch stream: "
+                              "%d launches of each kernel spread over the %d timed steps"
+                              % ("stamped by the kernel dispatch (hipExtLaunchKernel)"
+                                 if a.event_mode == "launch" else
+                                 "recorded right before and after the call (hipEventRecord)",
+                                 ns, a.steps)),
             "kernels_gbs": {k: round(kbytes(k, n) * W / (v * 1e-3) / 1e9, 1) for k, v in kern.items()},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -147,6 +147,9 @@ int amph_time_next_launch(void* start_event, void* stop_event);
  * Not for host synchronisation with the work it follows. */
 int amph_timing_event_create(void** event);
 int amph_timing_event_destroy(void* event);
+/* Record a timing event on a stream (hipEventRecord): bracketing an amph_*
+ * call with two of these times it from the end of the work before it. */
+int amph_timing_event_record(void* event, void* stream);
 /* Milliseconds between two recorded, completed timing events. */
 int amph_timing_event_elapsed_ms(void* start_event, void* stop_event, float* ms);
 
