@@ -418,3 +418,11 @@ def test_timing_events_stamp_the_next_launch(ctx, F, torch):
     assert 0.0 < ms < 50.0
     assert int(ff0.item()) == int(ff1.item()) == A._lib.AMPH_NO_FAILURE
     assert torch.equal(y0, y1)
+    # the same call bracketed by events recorded on its stream
+    import ctypes as C
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert A._lib.lib.amph_timing_event_record(e0.handle, s) == 0
+    ctx.recombine_verify(odos)
+    assert A._lib.lib.amph_timing_event_record(e1.handle, s) == 0
+    torch.cuda.synchronize()
+    assert 0.0 < e0.elapsed_ms(e1) < 50.0
