@@ -95,13 +95,14 @@ def _load():
 
 lib = _load()
 
-EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count", "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_set_batch_words",
-            "amph_strerror", "amph_last_error", "amph_version", "amph_recombine_verify",
-            "amph_mask_input", "amph_recombine", "amph_verify", "amph_verify_message",
-            "amph_mask_words", "amph_to_gfp", "amph_from_gfp", "amph_convert_share",
-            "amph_odo_pre", "amph_open_diffs", "amph_odo_post", "amph_synth_odos",
-            "amph_synth_words", "amph_host_register", "amph_host_unregister",
-            "amph_time_next_launch", "amph_timing_event_create", "amph_timing_event_destroy", "amph_timing_event_record",
+EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count",
+            "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_set_batch_words", "amph_strerror",
+            "amph_last_error", "amph_version", "amph_recombine_verify", "amph_mask_input",
+            "amph_recombine", "amph_verify", "amph_verify_message", "amph_mask_words",
+            "amph_to_gfp", "amph_from_gfp", "amph_convert_share", "amph_odo_pre",
+            "amph_open_diffs", "amph_odo_post", "amph_synth_odos", "amph_synth_words",
+            "amph_host_register", "amph_host_unregister", "amph_time_next_launch",
+            "amph_timing_event_create", "amph_timing_event_destroy", "amph_timing_event_record",
             "amph_timing_event_elapsed_ms", "amph_base64_encode", "amph_base64_decode",
             "amph_base64_encode_words", "amph_base64_decode_words", "amph_exchange_max_chars",
             "amph_exchange_encode", "amph_exchange_decode"]
