@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <initializer_list>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -450,10 +451,27 @@ const uint8_t* odo_field(const amph_odo& o, int k) {
   }
 }
 
+// Device-pointer word arrays are read and written as 16-byte vectors
+// (global_load/store_dwordx4), so every one must be 16-byte aligned.
+int check_dev_words(std::initializer_list<const void*> ptrs) {
+  for (const void* p : ptrs)
+    if (p && ((uintptr_t)p & 15))
+      return fail(AMPH_E_PARAM, "device word arrays must be 16-byte aligned");
+  return AMPH_OK;
+}
+
+int check_dev_odos(const amph_odo* odos, int n) {
+  for (int j = 0; j < n; ++j)
+    for (int k = 0; k < 5; ++k)
+      if (int st = check_dev_words({odo_field(odos[j], k)})) return st;
+  return AMPH_OK;
+}
+
 // device-mode first-fail: reset to the sentinel on the caller's stream,
 // unless the caller accumulates (AMPH_F_ACCUMULATE: min-combine into it)
 int reset_ff_dev(int64_t* ff, uint32_t flags, hipStream_t s) {
   if (!ff) return fail(AMPH_E_PARAM, "first_fail is required");
+  if ((uintptr_t)ff & 7) return fail(AMPH_E_PARAM, "first_fail must be 8-byte aligned");
   if (!(flags & AMPH_F_ACCUMULATE)) HIP_TRY(hipMemsetAsync(ff, 0x7F, sizeof(int64_t), s));
   return AMPH_OK;
 }
@@ -594,6 +612,8 @@ int amph_recombine_verify(amph_ctx* c, const amph_odo* odos, int n, uint8_t* out
   if (int st = odo_words(odos, n, &W)) return st;
   if (W && !out_secrets) return fail(AMPH_E_PARAM, "null output");
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_odos(odos, n)) return st;
+    if (int st = check_dev_words({out_secrets})) return st;
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipSetDevice(c->device));
     if (int st = reset_ff_dev(first_fail, flags, s)) return st;
@@ -628,6 +648,8 @@ int amph_mask_input(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* sec
     return fail(AMPH_E_LEN, "more secret words than verified input masks");
   if (n_secrets && (!secrets || !out_masked)) return fail(AMPH_E_PARAM, "null secrets/output");
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_odos(odos, n)) return st;
+    if (int st = check_dev_words({secrets, out_masked})) return st;
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipSetDevice(c->device));
     if (int st = reset_ff_dev(first_fail, flags, s)) return st;
@@ -681,6 +703,9 @@ int amph_recombine(amph_ctx* c, const uint8_t* const* shares, int n, size_t nbyt
   for (int j = 0; j < n; ++j)
     if (W && !shares[j]) return fail(AMPH_E_PARAM, "null share array");
   if (flags & AMPH_F_DEVICE) {
+    for (int j = 0; j < n; ++j)
+      if (int st = check_dev_words({shares[j]})) return st;
+    if (int st = check_dev_words({out})) return st;
     HIP_TRY(hipSetDevice(c->device));
     amph::ShareSet set{};
     for (int j = 0; j < n; ++j) set.s[j] = (const uint4*)shares[j];
@@ -705,6 +730,7 @@ int amph_verify(amph_ctx* c, const uint8_t* y, const uint8_t* r, const uint8_t* 
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (words && (!y || !r || !u || !v || !w)) return fail(AMPH_E_PARAM, "null input");
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_words({y, r, u, v, w})) return st;
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipSetDevice(c->device));
     if (int st = reset_ff_dev(first_fail, flags, s)) return st;
@@ -750,6 +776,7 @@ int amph_convert_share(amph_ctx* c, const uint8_t* masked, const uint8_t* tuples
   // [alpha] = alpha R mod p, computed once per call on the host
   const W4 alpha = amph::mont_mul(w4_of(ld128(mac_key_le)), amph::r2_word(c->f), c->f);
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_words({masked, tuples, out})) return st;
     HIP_TRY(hipSetDevice(c->device));
     hipError_t e = amph::launch_convert_share((const uint4*)masked, (const uint4*)tuples, words,
                                               alpha, use_zero, (uint4*)out, c->f,
@@ -776,6 +803,7 @@ int amph_odo_pre(amph_ctx* c, const uint8_t* share_data, size_t share_stride,
     return fail(AMPH_E_PARAM, "null buffer");
   const int sw = (int)(share_stride / 16);
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_words({share_data, masks, triples, oy, orr, ov, omag})) return st;
     HIP_TRY(hipSetDevice(c->device));
     hipError_t e = amph::launch_odo_pre((const uint4*)share_data, sw, (const uint4*)masks,
                                         (const uint4*)triples, words, (uint4*)oy, (uint4*)orr,
@@ -804,6 +832,9 @@ int amph_open_diffs(amph_ctx* c, const uint8_t* const* mags, const uint8_t* cons
   for (int j = 0; j < n; ++j)
     if (W && (!mags[j] || !negs[j])) return fail(AMPH_E_PARAM, "null diff array");
   if (flags & AMPH_F_DEVICE) {
+    for (int j = 0; j < n; ++j)
+      if (int st = check_dev_words({mags[j]})) return st;
+    if (int st = check_dev_words({out})) return st;
     HIP_TRY(hipSetDevice(c->device));
     amph::SignedSet set{};
     for (int j = 0; j < n; ++j) {
@@ -834,6 +865,7 @@ int amph_odo_post(amph_ctx* c, const uint8_t* opened, const uint8_t* triples, si
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (words && (!opened || !triples || !ow || !ou)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_words({opened, triples, ow, ou})) return st;
     HIP_TRY(hipSetDevice(c->device));
     hipError_t e = amph::launch_odo_post((const uint4*)opened, (const uint4*)triples, words,
                                          is_player0, (uint4*)ow, (uint4*)ou, c->f,
@@ -855,6 +887,7 @@ int amph_to_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, uint
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (words && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_words({in, out})) return st;
     HIP_TRY(hipSetDevice(c->device));
     hipError_t e = amph::launch_to_gfp((const uint4*)in, words, (uint4*)out, c->f, cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_to_gfp");
@@ -872,6 +905,7 @@ int amph_from_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, ui
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (words && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_words({in, out})) return st;
     HIP_TRY(hipSetDevice(c->device));
     hipError_t e = amph::launch_from_gfp((const uint4*)in, words, (uint4*)out, c->f, cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_from_gfp");
@@ -889,6 +923,7 @@ int amph_mask_words(amph_ctx* c, const uint8_t* secrets, const uint8_t* masks, s
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (words && (!secrets || !masks || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_words({secrets, masks, out})) return st;
     HIP_TRY(hipSetDevice(c->device));
     hipError_t e = amph::launch_mask_words((const uint4*)secrets, (const uint4*)masks, words,
                                            (uint4*)out, c->f, cfg(c, (hipStream_t)stream, words));

@@ -41,7 +41,9 @@
  * (including first_fail) is a DEVICE pointer on the context's device, the call
  * only enqueues work on `stream` (a hipStream_t, NULL = default stream) and
  * returns; first_fail then holds AMPH_NO_FAILURE or the failing index once the
- * stream reaches that point.
+ * stream reaches that point.  Device word arrays (16-byte words, tuples,
+ * diff magnitudes) must be 16-byte aligned and first_fail 8-byte aligned
+ * (AMPH_E_PARAM otherwise): the kernels move them as 16-byte vectors.
  *
  * Threading: host-pointer calls on one context are serialised by an internal
  * mutex; device-pointer calls use no context state and may run concurrently.

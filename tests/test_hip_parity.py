@@ -426,3 +426,26 @@ def test_timing_events_stamp_the_next_launch(ctx, F, torch):
     assert A._lib.lib.amph_timing_event_record(e1.handle, s) == 0
     torch.cuda.synchronize()
     assert 0.0 < e0.elapsed_ms(e1) < 50.0
+
+
+def test_device_arrays_must_be_aligned(ctx, torch):
+    """Device-pointer word arrays are moved as 16-byte vectors: a misaligned
+    one is rejected with AMPH_E_PARAM before any launch, an aligned view of
+    the same storage works."""
+    import amphora_amd as A
+    W = 1000
+    raw = torch.zeros(5 * 2 * W * 16 + 64, dtype=torch.uint8, device="cuda")
+    odd = raw[8:8 + 5 * 2 * W * 16].view(5, 2, W, 16)   # 8-byte aligned only
+    even = raw[16:16 + 5 * 2 * W * 16].view(5, 2, W, 16)
+    for buf, ok in ((odd, False), (even, True)):
+        odos = [tuple(buf[k, j] for k in range(5)) for j in range(2)]
+        if ok:
+            y, ff = ctx.recombine_verify(odos)
+            torch.cuda.synchronize()
+            assert y.shape == (W, 16)
+        else:
+            with pytest.raises(A._lib.AmphoraNativeError, match="16-byte aligned"):
+                ctx.recombine_verify(odos)
+    secrets = raw[24:24 + 16 * W].view(W, 16)
+    with pytest.raises(A._lib.AmphoraNativeError, match="16-byte aligned"):
+        ctx.to_gfp(secrets)
