@@ -460,6 +460,13 @@ int check_dev_words(std::initializer_list<const void*> ptrs) {
   return AMPH_OK;
 }
 
+// 24-character base64 records move as 8-byte vectors
+int check_dev_records(const void* p) {
+  if (p && ((uintptr_t)p & 7))
+    return fail(AMPH_E_PARAM, "device base64 record arrays must be 8-byte aligned");
+  return AMPH_OK;
+}
+
 int check_dev_odos(const amph_odo* odos, int n) {
   for (int j = 0; j < n; ++j)
     for (int k = 0; k < 5; ++k)
@@ -1051,6 +1058,8 @@ int amph_base64_encode_words(amph_ctx* c, const uint8_t* words16, size_t words, 
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (words && (!words16 || !out24)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_words({words16})) return st;
+    if (int st = check_dev_records(out24)) return st;
     HIP_TRY(hipSetDevice(c->device));
     hipError_t e = amph::launch_b64_words((const uint4*)words16, words, out24, cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_b64_words");
@@ -1068,6 +1077,8 @@ int amph_base64_decode_words(amph_ctx* c, const char* in24, size_t words, uint8_
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (words && (!in24 || !out16)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_words({out16})) return st;
+    if (int st = check_dev_records(in24)) return st;
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipSetDevice(c->device));
     if (int st = reset_ff_dev(bad_index, flags, s)) return st;
@@ -1121,6 +1132,7 @@ int amph_exchange_encode(amph_ctx* c, const uint8_t* mag16, const uint8_t* neg, 
   HIP_TRY(hipSetDevice(c->device));
   const size_t maxb = amph::xenc_max_bytes(npairs);
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_words({mag16})) return st;
     if (out_cap < maxb) return fail(AMPH_E_LEN, "output capacity below amph_exchange_max_chars(npairs)");
     hipStream_t s = (hipStream_t)stream;
     AsyncBuf scratch;
@@ -1163,6 +1175,7 @@ int amph_exchange_decode(amph_ctx* c, const char* text, size_t len, size_t npair
   if ((len && !text) || (npairs && (!mag16 || !neg))) return fail(AMPH_E_PARAM, "null buffer");
   HIP_TRY(hipSetDevice(c->device));
   if (flags & AMPH_F_DEVICE) {
+    if (int st = check_dev_words({mag16})) return st;
     hipStream_t s = (hipStream_t)stream;
     if (int st = reset_ff_dev(bad_index, flags, s)) return st;
     AsyncBuf scratch;

@@ -449,3 +449,8 @@ def test_device_arrays_must_be_aligned(ctx, torch):
     secrets = raw[24:24 + 16 * W].view(W, 16)
     with pytest.raises(A._lib.AmphoraNativeError, match="16-byte aligned"):
         ctx.to_gfp(secrets)
+    with pytest.raises(A._lib.AmphoraNativeError, match="16-byte aligned"):
+        ctx.base64_encode_words(secrets)
+    rec = raw[4:4 + 24 * 100].view(100, 24)  # 4-byte aligned records
+    with pytest.raises((A._lib.AmphoraNativeError, ValueError), match="8-byte aligned"):
+        ctx.base64_decode_words(rec)
