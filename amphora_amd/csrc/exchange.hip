@@ -326,15 +326,15 @@ __device__ __forceinline__ uint32_t count_starts32(const uint32_t (&w)[8], uint3
   return n;
 }
 
-constexpr int kDecBlock = 512;                         // threads per workgroup
-constexpr size_t kDecSpan = (size_t)kDecBlock * kDecBytes;  // 16 KiB of text per workgroup
+constexpr int kDecBlock = 256;  // threads per workgroup (512: parse 574 us, 256: 486, 128: 527 at 8 Mi pairs)
+constexpr size_t kDecSpan = (size_t)kDecBlock * kDecBytes;  // 8 KiB of text per workgroup
 constexpr int kWinPad = 256;                           // window context either side
 constexpr int kWin = (int)kDecSpan + 2 * kWinPad;      // staged bytes
 
-// Pass 1: number starts per 16 KiB span.  256 lanes x 64 bytes (four 16-B
+// Pass 1: number starts per 8 KiB span.  128 lanes x 64 bytes (four 16-B
 // loads in flight per lane, nontemporal: the text is read once here and once
 // by the parse), a wave reduction and one LDS word per wave.
-constexpr int kCntBlock = 256;
+constexpr int kCntBlock = 128;
 constexpr int kCntBytes = (int)(kDecSpan / kCntBlock);  // 64
 static_assert(kCntBytes == 64, "count lanes read four 16-B chunks");
 
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(kCntBlock) void k_xdec_count(Text t, uint64_t* bsum
   }
 }
 
-// The workgroup's 16 KiB plus kWinPad bytes either side, staged in LDS;
+// The workgroup's 8 KiB span plus kWinPad bytes either side, staged in LDS;
 // bytes outside it (long whitespace runs) come from global memory.
 struct Window {
   Text t;
@@ -534,9 +534,9 @@ __device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, boo
 // end, its key, and (member 1) where the text before its ',' ends; phase 2
 // ties each member 1 to the member 0 before it (same ',', other key), so
 // together they cover every byte of a well-formed array.  A well-formed text
-// has at most kMaxStarts numbers per 16 KiB ({"a":1,"b":2}, = 14 bytes per 2);
+// has at most kMaxStarts numbers per 8 KiB span ({"a":1,"b":2}, = 14 bytes per 2);
 // a start beyond that is reported as malformed.
-constexpr int kMaxStarts = 2560;
+constexpr int kMaxStarts = 1280;
 
 __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint64_t* bscan,
                                                       size_t nvals, uint4* mag, uint8_t* neg,
