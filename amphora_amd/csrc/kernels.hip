@@ -167,7 +167,7 @@ __device__ __forceinline__ void stage_tuples(uint4* lds, const uint4* src, size_
   }
 }
 
-constexpr int kPairBlock = 256;  // pairs per workgroup of the LDS-staged kernels
+constexpr int kPairBlock = 128;  // pairs per workgroup of the LDS-staged kernels (256: 1-2 % slower at 16 Mi, 512: 2-12 %)
 
 // K_CONV, one word per lane; the workgroup's input-mask tuples (value||mac,
 // 32 B) come in and its output shares (value||mac) go out as coalesced 16-B
