@@ -10,9 +10,10 @@
 //     [{"a":10,"b":25},{"a":-39,"b":24},...]
 //
 // Encode (diffs -> compact array text, byte-identical to Jackson's default
-// output): a length pass, a device-wide exclusive scan of the entry lengths,
-// and a write pass that formats each workgroup's entries into LDS and stores
-// the contiguous run with aligned 4-byte stores.
+// output): a pass that sums each workgroup's entry lengths, a scan of those
+// sums, and a write pass that places its entries with a workgroup scan,
+// formats them into LDS and stores the contiguous run with aligned 16-byte
+// stores.
 //
 // Decode (array text -> diffs): every lane classifies 32 bytes; number starts
 // are counted per workgroup, scanned, and each start is parsed by the lane
@@ -22,8 +23,8 @@
 // validated without a second pass; the first malformed byte's offset is
 // reported.  Whitespace between tokens is accepted, as in any JSON reader.
 //
-// Decimal conversion: 128-bit magnitude <-> five base-10^9 chunks (four
-// 64-by-32-bit divisions by a constant per chunk), chunks <-> digits.
+// Decimal conversion: 128-bit magnitude <-> five base-10^9 chunks (nine
+// 64-by-32-bit divisions by a constant in all, to_chunks), chunks <-> digits.
 #include <hip/hip_ext.h>
 
 #include "kernels.hpp"
@@ -43,18 +44,6 @@ constexpr int kScanBlock = 1024;  // elements per workgroup of the scan passes
 constexpr int kDecBytes = 32;     // text bytes per lane (decode)
 constexpr uint64_t kE9 = 1000000000ull;
 
-__device__ __forceinline__ uint32_t divmod_e9(uint32_t (&v)[4]) {
-  uint64_t rem = 0;
-#pragma unroll
-  for (int i = 3; i >= 0; --i) {
-    const uint64_t cur = (rem << 32) | v[i];
-    const uint64_t q = cur / kE9;  // < 2^32: rem < 10^9
-    rem = cur - q * kE9;
-    v[i] = (uint32_t)q;
-  }
-  return (uint32_t)rem;
-}
-
 __device__ __forceinline__ int ndigits32(uint32_t x) {  // x < 10^9; 0 -> 1
   int n = 1;
 #pragma unroll
@@ -62,12 +51,38 @@ __device__ __forceinline__ int ndigits32(uint32_t x) {  // x < 10^9; 0 -> 1
   return n;
 }
 
+// One base-2^32 long-division step by 10^9: (rem, x) -> quotient, rem updated.
+__device__ __forceinline__ uint32_t div_step_e9(uint64_t& rem, uint32_t x) {
+  const uint64_t cur = (rem << 32) | x;
+  const uint64_t q = cur / kE9;  // < 2^32: rem < 10^9
+  rem = cur - q * kE9;
+  return (uint32_t)q;
+}
+
 // 128-bit magnitude -> base-10^9 chunks (little end first); returns the
-// decimal digit count (1 for zero).
+// decimal digit count (1 for zero).  Any x < 2^128 leaves x / 10^9 < 2^98.1,
+// x / 10^18 < 2^68.2, x / 10^27 < 2^38.3 and x / 10^36 < 2^8.4, so after
+// each round the leading limb is known to be below 10^9 (it becomes the
+// next round's starting remainder with no division) and one more limb is
+// zero: 9 64-bit divisions + 1 32-bit one instead of 5 rounds x 4.
 __device__ __forceinline__ int to_chunks(const uint4& m, uint32_t (&ch)[5]) {
-  uint32_t v[4] = {m.x, m.y, m.z, m.w};
-#pragma unroll
-  for (int k = 0; k < 5; ++k) ch[k] = divmod_e9(v);
+  uint64_t rem = 0;
+  const uint32_t a3 = m.w / (uint32_t)kE9;  // < 5
+  rem = m.w - a3 * (uint32_t)kE9;
+  const uint32_t a2 = div_step_e9(rem, m.z), a1 = div_step_e9(rem, m.y);
+  const uint32_t a0 = div_step_e9(rem, m.x);
+  ch[0] = (uint32_t)rem;
+  rem = a3;  // x / 10^9 = (a3, a2, a1, a0) < 2^98.1
+  const uint32_t b2 = div_step_e9(rem, a2), b1 = div_step_e9(rem, a1);
+  const uint32_t b0 = div_step_e9(rem, a0);
+  ch[1] = (uint32_t)rem;
+  rem = b2;  // x / 10^18 = (b2, b1, b0) < 2^68.2
+  const uint32_t c1 = div_step_e9(rem, b1), c0 = div_step_e9(rem, b0);
+  ch[2] = (uint32_t)rem;
+  rem = c1;  // x / 10^27 = (c1, c0) < 2^38.3
+  const uint32_t d0 = div_step_e9(rem, c0);
+  ch[3] = (uint32_t)rem;
+  ch[4] = d0;  // x / 10^36 < 2^8.4
   int top = 0;
 #pragma unroll
   for (int k = 1; k < 5; ++k) top = ch[k] ? k : top;
@@ -97,10 +112,8 @@ __device__ __forceinline__ uint32_t ascii4(uint32_t x) {
   return 0x30303030u | a1 | ((a - 10u * a1) << 8) | (b1 << 16) | ((b - 10u * b1) << 24);
 }
 
-__device__ __forceinline__ char* put_int(char* o, const uint4& m, bool neg) {
-  uint32_t ch[5];
-  const int nd = to_chunks(m, ch);
-  if (neg && !is_zero(m)) *o++ = '-';  // BigInteger has no negative zero
+// nd decimal digits of the chunks ch (to_chunks) at o; returns o + nd.
+__device__ __forceinline__ char* put_digits(char* o, const uint32_t (&ch)[5], int nd) {
   // chunk k (base 10^9, little end first) holds text positions
   // [nd - 9 (k + 1), nd - 9 k); its 9 digits come from one division by 10^8,
   // one by 10^4 and two 4-digit SWAR conversions instead of 9 divisions by 10
@@ -119,14 +132,6 @@ __device__ __forceinline__ char* put_int(char* o, const uint4& m, bool neg) {
       if (base + j >= 0) o[base + j] = (char)dig[j];
   }
   return o + nd;
-}
-
-__global__ __launch_bounds__(kMaxBlock) void k_xenc_len(const uint4* mag, const uint8_t* neg,
-                                                    size_t npairs, uint64_t* lens) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < npairs; k += stride)
-    lens[k] = (uint64_t)entry_len(mag[2 * k], neg[2 * k] != 0, mag[2 * k + 1], neg[2 * k + 1] != 0,
-                                  k + 1 == npairs);
 }
 
 // ---- device-wide exclusive scan of u64 (three passes) ----------------------------
@@ -193,42 +198,75 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_apply(uint64_t* x, size_t n
   if (blockIdx.x == 0 && threadIdx.x == 0) x[n] = bsum[nb];
 }
 
-// Entries of one workgroup formatted into LDS, then stored as one contiguous
-// run: aligned 4-byte words in the middle, single bytes at the two ends.
+// Encode pass 1: the text length of each workgroup's run of entries
+// (bs[g] = sum of entry_len over pairs [256 g, 256 g + 256)).
+__global__ __launch_bounds__(kXBlock) void k_xenc_bsum(const uint4* mag, const uint8_t* neg,
+                                                   size_t npairs, uint64_t* bs) {
+  const size_t k = (size_t)blockIdx.x * kXBlock + threadIdx.x;
+  uint64_t len = 0, total;
+  if (k < npairs)
+    len = (uint64_t)entry_len(mag[2 * k], neg[2 * k] != 0, mag[2 * k + 1], neg[2 * k + 1] != 0,
+                              k + 1 == npairs);
+  block_excl_scan(len, &total);
+  if (threadIdx.x == 0) bs[blockIdx.x] = total;
+}
+
+// Encode pass 3 (after the scan of bs): each lane converts its two numbers,
+// the workgroup scans the entry lengths to place them, and the entries are
+// formatted into LDS and stored as one contiguous run.  The run sits in LDS
+// at the same offset mod 16 as its destination (sh), so every 16-byte unit
+// wholly inside it moves as one aligned ds_read_b128 + global 16-byte store;
+// the up to 15 bytes at either end go out singly.
 __global__ __launch_bounds__(kXBlock) void k_xenc_write(const uint4* mag, const uint8_t* neg,
-                                                    size_t npairs, const uint64_t* offs,
-                                                    char* out, unsigned long long* out_len) {
-  __shared__ char buf[kXBlock * kXEntry + 8];
-  const size_t k0 = (size_t)blockIdx.x * kXBlock, k = k0 + threadIdx.x;
-  const size_t kend = min(k0 + (size_t)kXBlock, npairs);
-  const uint64_t base = offs[k0], end = offs[kend];
+                                                    size_t npairs, const uint64_t* bs,
+                                                    size_t nblocks, char* out,
+                                                    unsigned long long* out_len) {
+  __shared__ uint4 bufv[(kXBlock * kXEntry + 8) / 16 + 2];
+  char* buf = reinterpret_cast<char*>(bufv);
+  const size_t k = (size_t)blockIdx.x * kXBlock + threadIdx.x;
+  uint32_t cd[5], ce[5];
+  int nd = 0, ne = 0;
+  bool sd = false, se = false;
+  uint64_t len = 0, total;
   if (k < npairs) {
-    char* o = buf + (offs[k] - base);
+    const uint4 d = mag[2 * k], e = mag[2 * k + 1];
+    nd = to_chunks(d, cd);
+    ne = to_chunks(e, ce);
+    sd = neg[2 * k] != 0 && !is_zero(d);  // BigInteger has no negative zero
+    se = neg[2 * k + 1] != 0 && !is_zero(e);
+    len = 11 + nd + sd + ne + se + (k + 1 < npairs);
+  }
+  const uint64_t loc = block_excl_scan(len, &total);
+  const uint64_t base = bs[blockIdx.x];
+  char* dst = out + 1 + base;  // out[0] = '['
+  const size_t sh = (uintptr_t)dst & 15;
+  if (k < npairs) {
+    char* o = buf + sh + loc;
     o = put_str(o, "{\"a\":");
-    o = put_int(o, mag[2 * k], neg[2 * k] != 0);
+    if (sd) *o++ = '-';
+    o = put_digits(o, cd, nd);
     o = put_str(o, ",\"b\":");
-    o = put_int(o, mag[2 * k + 1], neg[2 * k + 1] != 0);
+    if (se) *o++ = '-';
+    o = put_digits(o, ce, ne);
     *o++ = '}';
     if (k + 1 < npairs) *o = ',';
   }
   __syncthreads();
-  char* dst = out + 1 + base;  // out[0] = '['
-  const size_t n = end - base;
-  const size_t head = min(n, (size_t)((4 - ((uintptr_t)dst & 3)) & 3));
-  const size_t nw = (n - head) / 4;
-  if (threadIdx.x < head) dst[threadIdx.x] = buf[threadIdx.x];
-  for (size_t w = threadIdx.x; w < nw; w += kXBlock) {
-    const char* s = buf + head + 4 * w;
-    const uint32_t v = (uint32_t)(uint8_t)s[0] | ((uint32_t)(uint8_t)s[1] << 8) |
-                       ((uint32_t)(uint8_t)s[2] << 16) | ((uint32_t)(uint8_t)s[3] << 24);
-    *reinterpret_cast<uint32_t*>(dst + head + 4 * w) = v;
+  char* dal = dst - sh;  // 16-aligned; bytes [sh, sh + total) of it are this run
+  const size_t endb = sh + total;
+  const size_t ulo = sh ? 1 : 0, uhi = endb / 16;  // whole 16-byte units [ulo, uhi)
+  if (uhi <= ulo) {
+    if (sh + threadIdx.x < endb) dal[sh + threadIdx.x] = buf[sh + threadIdx.x];
+  } else {
+    if (sh + threadIdx.x < 16 * ulo) dal[sh + threadIdx.x] = buf[sh + threadIdx.x];
+    for (size_t u = ulo + threadIdx.x; u < uhi; u += kXBlock)
+      reinterpret_cast<uint4*>(dal)[u] = bufv[u];
+    if (16 * uhi + threadIdx.x < endb) dal[16 * uhi + threadIdx.x] = buf[16 * uhi + threadIdx.x];
   }
-  const size_t t0 = head + 4 * nw;
-  if (threadIdx.x < n - t0) dst[t0 + threadIdx.x] = buf[t0 + threadIdx.x];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     out[0] = '[';
-    out[1 + offs[npairs]] = ']';
-    if (out_len) *out_len = offs[npairs] + 2;
+    out[1 + bs[nblocks]] = ']';
+    if (out_len) *out_len = bs[nblocks] + 2;
   }
 }
 
@@ -719,28 +757,34 @@ hipError_t scan_u64(uint64_t* x, size_t n, uint64_t* bsum, LaunchCfg c) {
 }  // namespace
 
 size_t xenc_scratch_bytes(size_t npairs) {
-  return 8 * (npairs + 1) + 8 * ((size_t)blocks_of(npairs, kScanBlock) + 1);
+  const size_t nb = blocks_of(npairs, kXBlock);
+  return 8 * (nb + 1) + 8 * ((size_t)blocks_of(nb, kScanBlock) + 1);
 }
 
 size_t xenc_max_bytes(size_t npairs) { return (size_t)kXEntry * npairs + 2; }
 
+// Three passes: per-workgroup text lengths (k_xenc_bsum), a scan of those
+// (one u64 per 256 pairs), then k_xenc_write, which recomputes its entries'
+// lengths while converting and places them with a workgroup scan -- no
+// per-pair length or offset array goes through HBM.
 hipError_t launch_exchange_encode(const uint4* mag, const uint8_t* neg, size_t npairs, char* out,
                                   unsigned long long* out_len, void* scratch, const LaunchCfg& c) {
-  uint64_t* offs = static_cast<uint64_t*>(scratch);
-  uint64_t* bsum = offs + npairs + 1;
+  const size_t nb = npairs ? blocks_of(npairs, kXBlock) : 0;
+  uint64_t* bs = static_cast<uint64_t*>(scratch);
+  uint64_t* tmp = bs + nb + 1;
   LaunchCfg c0 = c, cm = c, c1 = c;
   c0.ev_stop = nullptr;
   cm.ev_start = cm.ev_stop = nullptr;
   c1.ev_start = nullptr;
-  if (npairs > 0) {
-    AMPH_LAUNCH(k_xenc_len, dim3(blocks_of(npairs, kMaxBlock)), dim3(kMaxBlock), c0, mag, neg, npairs, offs);
-    hipError_t e = scan_u64(offs, npairs, bsum, cm);
+  if (nb > 0) {
+    AMPH_LAUNCH(k_xenc_bsum, dim3((unsigned)nb), dim3(kXBlock), c0, mag, neg, npairs, bs);
+    hipError_t e = scan_u64(bs, nb, tmp, cm);
     if (e != hipSuccess) return e;
   } else {
-    AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c0, offs, (size_t)0);
+    AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c0, bs, (size_t)0);
   }
-  AMPH_LAUNCH(k_xenc_write, dim3(npairs ? blocks_of(npairs, kXBlock) : 1), dim3(kXBlock), c1, mag, neg,
-              npairs, offs, out, out_len);
+  AMPH_LAUNCH(k_xenc_write, dim3(nb ? (unsigned)nb : 1u), dim3(kXBlock), c1, mag, neg, npairs, bs,
+              nb, out, out_len);
   return hipGetLastError();
 }
 
