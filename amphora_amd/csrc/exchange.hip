@@ -124,6 +124,12 @@ __device__ __forceinline__ char* put_digits(char* o, const uint32_t (&ch)[5], in
     const uint32_t c = ch[k], top = c / 100000000u, r = c - top * 100000000u;
     const uint32_t hi = r / 10000u;
     const uint32_t w0 = ascii4(hi), w1 = ascii4(r - hi * 10000u);
+    if (base >= 0) {  // a whole chunk: 1 byte + two (unaligned) 4-byte LDS stores
+      o[base] = (char)(0x30u + top);
+      __builtin_memcpy(o + base + 1, &w0, 4);
+      __builtin_memcpy(o + base + 5, &w1, 4);
+      continue;
+    }
     const uint32_t dig[9] = {0x30u + top,      w0 & 0xFFu,         (w0 >> 8) & 0xFFu,
                              (w0 >> 16) & 0xFFu, w0 >> 24,          w1 & 0xFFu,
                              (w1 >> 8) & 0xFFu,  (w1 >> 16) & 0xFFu, w1 >> 24};
