@@ -91,14 +91,68 @@ __device__ __forceinline__ int to_chunks(const uint4& m, uint32_t (&ch)[5]) {
 
 __device__ __forceinline__ bool is_zero(const uint4& m) { return (m.x | m.y | m.z | m.w) == 0; }
 
-// {"a":A,"b":B}  (+ ',' unless last)
-__device__ __forceinline__ int entry_len(const uint4& d, bool nd, const uint4& e, bool ne,
-                                         bool last) {
-  uint32_t ch[5];
-  const int ld = to_chunks(d, ch) + (nd && !is_zero(d));
-  const int le = to_chunks(e, ch) + (ne && !is_zero(e));
-  return 11 + ld + le + (last ? 0 : 1);
+// 10^0 .. 10^38 as 128-bit little-endian limbs (10^38 < 2^128 < 10^39)
+__device__ const uint32_t kPow10[39][4] = {
+    {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x0000000au, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x00000064u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x000003e8u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x00002710u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x000186a0u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x000f4240u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x00989680u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x05f5e100u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x3b9aca00u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x540be400u, 0x00000002u, 0x00000000u, 0x00000000u},
+    {0x4876e800u, 0x00000017u, 0x00000000u, 0x00000000u},
+    {0xd4a51000u, 0x000000e8u, 0x00000000u, 0x00000000u},
+    {0x4e72a000u, 0x00000918u, 0x00000000u, 0x00000000u},
+    {0x107a4000u, 0x00005af3u, 0x00000000u, 0x00000000u},
+    {0xa4c68000u, 0x00038d7eu, 0x00000000u, 0x00000000u},
+    {0x6fc10000u, 0x002386f2u, 0x00000000u, 0x00000000u},
+    {0x5d8a0000u, 0x01634578u, 0x00000000u, 0x00000000u},
+    {0xa7640000u, 0x0de0b6b3u, 0x00000000u, 0x00000000u},
+    {0x89e80000u, 0x8ac72304u, 0x00000000u, 0x00000000u},
+    {0x63100000u, 0x6bc75e2du, 0x00000005u, 0x00000000u},
+    {0xdea00000u, 0x35c9adc5u, 0x00000036u, 0x00000000u},
+    {0xb2400000u, 0x19e0c9bau, 0x0000021eu, 0x00000000u},
+    {0xf6800000u, 0x02c7e14au, 0x0000152du, 0x00000000u},
+    {0xa1000000u, 0x1bceccedu, 0x0000d3c2u, 0x00000000u},
+    {0x4a000000u, 0x16140148u, 0x00084595u, 0x00000000u},
+    {0xe4000000u, 0xdcc80cd2u, 0x0052b7d2u, 0x00000000u},
+    {0xe8000000u, 0x9fd0803cu, 0x033b2e3cu, 0x00000000u},
+    {0x10000000u, 0x3e250261u, 0x204fce5eu, 0x00000000u},
+    {0xa0000000u, 0x6d7217cau, 0x431e0faeu, 0x00000001u},
+    {0x40000000u, 0x4674edeau, 0x9f2c9cd0u, 0x0000000cu},
+    {0x80000000u, 0xc0914b26u, 0x37be2022u, 0x0000007eu},
+    {0x00000000u, 0x85acef81u, 0x2d6d415bu, 0x000004eeu},
+    {0x00000000u, 0x38c15b0au, 0xc6448d93u, 0x0000314du},
+    {0x00000000u, 0x378d8e64u, 0xbead87c0u, 0x0001ed09u},
+    {0x00000000u, 0x2b878fe8u, 0x72c74d82u, 0x00134261u},
+    {0x00000000u, 0xb34b9f10u, 0x7bc90715u, 0x00c097ceu},
+    {0x00000000u, 0x00f436a0u, 0xd5da46d9u, 0x0785ee10u},
+    {0x00000000u, 0x098a2240u, 0x5a86c47au, 0x4b3b4ca8u}};
+
+__device__ __forceinline__ bool ge128(const uint4& a, const uint32_t (&b)[4]) {
+  uint32_t br;
+  __builtin_subc(a.x, b[0], 0u, &br);
+  __builtin_subc(a.y, b[1], br, &br);
+  __builtin_subc(a.z, b[2], br, &br);
+  __builtin_subc(a.w, b[3], br, &br);
+  return br == 0;
 }
+
+// Decimal digit count of a 128-bit magnitude (1 for zero) without the
+// base-10^9 split: t = floor(bits * log10(2)) (bits * 1233 >> 12 is exact
+// for bits <= 128) is the count or one less, decided by one compare with 10^t.
+__device__ __forceinline__ int ndigits128(const uint4& m) {
+  const int bits = m.w ? 128 - __clz(m.w) : m.z ? 96 - __clz(m.z) : m.y ? 64 - __clz(m.y)
+                                                                   : 32 - __clz(m.x);
+  const int t = (bits * 1233) >> 12;
+  const int n = t + (ge128(m, kPow10[t]) ? 1 : 0);
+  return n ? n : 1;
+}
+
 
 __device__ __forceinline__ char* put_str(char* o, const char* s) {
   while (*s) *o++ = *s++;
@@ -205,16 +259,29 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_apply(uint64_t* x, size_t n
 }
 
 // Encode pass 1: the text length of each workgroup's run of entries
-// (bs[g] = sum of entry_len over pairs [256 g, 256 g + 256)).
-__global__ __launch_bounds__(kXBlock) void k_xenc_bsum(const uint4* mag, const uint8_t* neg,
-                                                   size_t npairs, uint64_t* bs) {
-  const size_t k = (size_t)blockIdx.x * kXBlock + threadIdx.x;
-  uint64_t len = 0, total;
+// (bs[g] = sum of the entry lengths of pairs [256 g, 256 g + 256)); digit
+// counts from the bit length (ndigits128), not the base-10^9 split.
+__global__ __launch_bounds__(4 * kXBlock) void k_xenc_bsum(const uint4* mag, const uint8_t* neg,
+                                                       size_t npairs, size_t nb, uint64_t* bs) {
+  // one pair per lane, 4 sub-blocks of 256 pairs per 1024-lane workgroup:
+  // wave sums by shuffles, then 4 lanes add their sub-block's 4 wave sums
+  __shared__ uint32_t ws[16];
+  const size_t k = (size_t)blockIdx.x * (4 * kXBlock) + threadIdx.x;
+  uint32_t len = 0;
   if (k < npairs)
-    len = (uint64_t)entry_len(mag[2 * k], neg[2 * k] != 0, mag[2 * k + 1], neg[2 * k + 1] != 0,
-                              k + 1 == npairs);
-  block_excl_scan(len, &total);
-  if (threadIdx.x == 0) bs[blockIdx.x] = total;
+  {  // {"a":A,"b":B} (+ ',' unless last)
+    const uint4 d = mag[2 * k], e = mag[2 * k + 1];
+    len = 11 + ndigits128(d) + (neg[2 * k] != 0 && !is_zero(d)) + ndigits128(e) +
+          (neg[2 * k + 1] != 0 && !is_zero(e)) + (k + 1 < npairs);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) len += __shfl_xor(len, o, 64);
+  if (__lane_id() == 0) ws[threadIdx.x >> 6] = len;
+  __syncthreads();
+  const size_t sub = 4 * (size_t)blockIdx.x + threadIdx.x;
+  if (threadIdx.x < 4 && sub < nb)
+    bs[sub] = (uint64_t)ws[4 * threadIdx.x] + ws[4 * threadIdx.x + 1] + ws[4 * threadIdx.x + 2] +
+              ws[4 * threadIdx.x + 3];
 }
 
 // Encode pass 3 (after the scan of bs): each lane converts its two numbers,
@@ -783,7 +850,7 @@ hipError_t launch_exchange_encode(const uint4* mag, const uint8_t* neg, size_t n
   cm.ev_start = cm.ev_stop = nullptr;
   c1.ev_start = nullptr;
   if (nb > 0) {
-    AMPH_LAUNCH(k_xenc_bsum, dim3((unsigned)nb), dim3(kXBlock), c0, mag, neg, npairs, bs);
+    AMPH_LAUNCH(k_xenc_bsum, dim3(blocks_of(nb, 4)), dim3(4 * kXBlock), c0, mag, neg, npairs, nb, bs);
     hipError_t e = scan_u64(bs, nb, tmp, cm);
     if (e != hipSuccess) return e;
   } else {
