@@ -160,10 +160,13 @@ __device__ __forceinline__ char* put_str(char* o, const char* s) {
 }
 
 // x < 10^4 -> its 4 ASCII digits, first digit in the lowest byte
+// (x / 100 as x * 5243 >> 19, exact below 43699; then both 2-digit halves
+// split by 10 at once in 16-bit fields: y * 103 >> 10 = y / 10 for y < 179)
 __device__ __forceinline__ uint32_t ascii4(uint32_t x) {
-  const uint32_t a = x / 100u, b = x - 100u * a;
-  const uint32_t a1 = a / 10u, b1 = b / 10u;
-  return 0x30303030u | a1 | ((a - 10u * a1) << 8) | (b1 << 16) | ((b - 10u * b1) << 24);
+  const uint32_t a = (x * 5243u) >> 19, b = x - 100u * a;
+  const uint32_t p = a | (b << 16);
+  const uint32_t q = ((p * 103u) >> 10) & 0x000F000Fu;
+  return 0x30303030u | q | ((p - 10u * q) << 8);
 }
 
 // nd decimal digits of the chunks ch (to_chunks) at o; returns o + nd.
