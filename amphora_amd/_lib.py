@@ -32,6 +32,13 @@ class AmphoraNativeError(RuntimeError):
         self.status = status
 
 
+def _need(cond: bool, detail: str):
+    """Host-side length check of a call whose C entry point takes raw pointers
+    and one word count (it cannot see the buffers' sizes)."""
+    if not cond:
+        raise AmphoraNativeError(AMPH_E_LEN, detail)
+
+
 _STATUS = {AMPH_E_VERIFY: "verification failed", AMPH_E_LEN: "length invariant",
            AMPH_E_PARAM: "invalid argument", AMPH_E_HIP: "HIP error", AMPH_E_NOMEM: "out of memory"}
 
@@ -241,6 +248,9 @@ class Context:
         views = []
         for j, o in enumerate(odos):
             fs = [words_view(f) for f in o]
+            if len(fs) != 5 or any(f.shape[0] != fs[0].shape[0] for f in fs):
+                # OutputDeliveryObject's constructor invariant (OutputDeliveryObject.java:90-96)
+                raise AmphoraNativeError(AMPH_E_LEN, "The provided shares must be of the same length")
             views.append(fs)
             nbytes = fs[0].shape[0] * 16
             arr[j] = _AmphOdo(*[_ptr(f) for f in fs], nbytes)
@@ -333,6 +343,7 @@ class Context:
     # -- service -------------------------------------------------------------
     def convert_share(self, masked16, tuples32, mac_key: int, use_zero_input_as_data: bool):
         m, t = words_view(masked16), words_view(tuples32, 32)
+        _need(t.shape[0] >= m.shape[0], "Received more input data than available inputMasks.")
         flags, stream = self._mode(m, t)
         out = self._empty(m, (m.shape[0], 32))
         self._check(lib.amph_convert_share(self._h, _ptr(m), _ptr(t), m.shape[0],
@@ -343,8 +354,11 @@ class Context:
     def odo_pre(self, share_data, share_stride: int, masks32, triples96):
         sd = words_view(share_data, share_stride)
         mk, tr = words_view(masks32, 32), words_view(triples96, 96)
-        flags, stream = self._mode(sd, mk, tr)
         W = sd.shape[0]
+        # 2 input masks and 2 triples per word (OutputDeliveryService.java:102-107,177-185)
+        _need(mk.shape[0] == 2 * W, "expected %d input-mask tuples, got %d" % (2 * W, mk.shape[0]))
+        _need(tr.shape[0] == 2 * W, "expected %d multiplication triples, got %d" % (2 * W, tr.shape[0]))
+        flags, stream = self._mode(sd, mk, tr)
         y, r, v = (self._empty(sd, (W, 16)) for _ in range(3))
         mag = self._empty(sd, (2 * W, 2, 16))
         neg = self._empty(sd, (2 * W, 2))
@@ -356,8 +370,13 @@ class Context:
     def open_diffs(self, mags, negs):
         ms = [m if _is_dev(m) else np.ascontiguousarray(m, np.uint8) for m in mags]
         ns = [n if _is_dev(n) else np.ascontiguousarray(n, np.uint8) for n in negs]
-        flags, stream = self._mode(*ms, *ns)
+        _need(len(ms) == len(ns) and len(ms) >= 1, "one (mag, neg) pair per party")
         n_pairs = ms[0].shape[0]
+        for m, n in zip(ms, ns):  # every party opens the same 2W pairs (recombineDiffs :231-272)
+            _need(tuple(m.shape) == (n_pairs, 2, 16) and tuple(n.shape) == (n_pairs, 2),
+                  "party diff lists differ in length: %s / %s vs %d pairs"
+                  % (tuple(m.shape), tuple(n.shape), n_pairs))
+        flags, stream = self._mode(*ms, *ns)
         out = self._empty(ms[0], (n_pairs, 2, 16))
         pm = (C.c_void_p * len(ms))(*[_ptr(x) for x in ms])
         pn = (C.c_void_p * len(ns))(*[_ptr(x) for x in ns])
@@ -367,6 +386,8 @@ class Context:
     def odo_post(self, opened, triples96, is_player0: bool):
         op = opened if _is_dev(opened) else np.ascontiguousarray(opened, np.uint8)
         tr = words_view(triples96, 96)
+        _need(tr.shape[0] % 2 == 0 and tuple(op.shape) == (tr.shape[0], 2, 16),
+              "opened values %s do not match %d triples" % (tuple(op.shape), tr.shape[0]))
         flags, stream = self._mode(op, tr)
         W = tr.shape[0] // 2
         w, u = self._empty(tr, (W, 16)), self._empty(tr, (W, 16))

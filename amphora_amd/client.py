@@ -144,6 +144,12 @@ def create_masked_input(util: SecretShareUtil, secret: Secret,
     arrays = _odo_arrays(mask_odos)
     W = arrays[0][0].shape[0]
     if secret.size() > W:
+        # the reference verifies every mask first (verifyOutputDeliveryObjects
+        # :153) and only then indexes inputMasks.get(i) past the end (:155-157):
+        # a tampered mask set fails verification before the size mismatch shows
+        _, ff = util.context.recombine_verify(arrays)
+        if ff >= 0:
+            _raise_for(util, arrays, ff)
         raise IndexError("Index %d out of bounds for length %d" % (W, W))
     masked, ff = util.context.mask_input(arrays, pack(secret.data, util.prime))
     if ff >= 0:

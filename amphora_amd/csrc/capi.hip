@@ -205,7 +205,7 @@ int host_threads() {
 template <class Launch>
 int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
                 const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
-                Launch& launch);
+                Launch& launch, size_t ff_scale);
 
 // Streams `words` through the device in batches of ctx->batch_words, one
 // HIP stream per engine: streams[0] carries every HtoD copy in batch order,
@@ -222,11 +222,13 @@ int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
 // one by CPU threads once its previous HtoD is done, pageable outputs out of
 // one once its previous DtoH is done.  Page-locked caller buffers are DMA'd
 // directly.  Verify failures land in one device word per batch; the smallest
-// global index is reported.
+// global index is reported.  A kernel reports its failure index in units of
+// 1/ff_scale of a batch word (the base64 stream decode: a character offset,
+// 16 characters per batch word), so batch b's base is b * bw * ff_scale.
 template <class Launch>
 int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
                      const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
-                     Launch& launch) {
+                     Launch& launch, size_t ff_scale) {
   if (first_fail) *first_fail = -1;
   if (words == 0) return AMPH_OK;
   constexpr int S = amph_ctx::kSlots;
@@ -352,7 +354,7 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
     HIP_TRY(hipMemcpy(h.data(), c->ff.p, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     for (size_t b = 0; b < nb; ++b) {
       if (h[b] != amph::kNoFail) {
-        if (first_fail) *first_fail = (int64_t)(b * bw + h[b]);
+        if (first_fail) *first_fail = (int64_t)(b * bw * ff_scale + h[b]);
         return AMPH_E_VERIFY;
       }
     }
@@ -366,9 +368,9 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
 template <class Launch>
 int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
                 const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
-                Launch&& launch) {
-  if (!c->sub.empty()) return run_sharded(c, words, ins, outs, with_ff, first_fail, launch);
-  const int rc = run_batched_impl(c, words, ins, outs, with_ff, first_fail, launch);
+                Launch&& launch, size_t ff_scale = 1) {
+  if (!c->sub.empty()) return run_sharded(c, words, ins, outs, with_ff, first_fail, launch, ff_scale);
+  const int rc = run_batched_impl(c, words, ins, outs, with_ff, first_fail, launch, ff_scale);
   if (rc != AMPH_OK && rc != AMPH_E_VERIFY) {
     for (int s = 0; s < amph_ctx::kSlots; ++s) {
       if (c->streams[s]) (void)hipStreamSynchronize(c->streams[s]);
@@ -384,7 +386,7 @@ int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
 template <class Launch>
 int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
                 const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
-                Launch& launch) {
+                Launch& launch, size_t ff_scale) {
   if (first_fail) *first_fail = -1;
   g_ev_start = g_ev_stop = nullptr;  // per-launch timing is single-device only
   if (words == 0) return AMPH_OK;
@@ -406,7 +408,7 @@ int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
       amph_ctx* s = g->sub[d];
       try {
         std::lock_guard<std::mutex> lk(s->mu);
-        res[d].st = run_batched(s, cnt, in2, out2, with_ff, &res[d].ff, launch);
+        res[d].st = run_batched(s, cnt, in2, out2, with_ff, &res[d].ff, launch, ff_scale);
       } catch (const std::exception& e) {
         res[d].st = fail(AMPH_E_NOMEM, e.what());
       }
@@ -418,7 +420,7 @@ int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
     if (res[d].st != AMPH_OK && res[d].st != AMPH_E_VERIFY) return fail(res[d].st, res[d].err);
   for (size_t d = 0; d < th.size(); ++d)
     if (res[d].st == AMPH_E_VERIFY) {
-      if (first_fail) *first_fail = (int64_t)(d * per) + res[d].ff;
+      if (first_fail) *first_fail = (int64_t)(d * per * ff_scale) + res[d].ff;
       return AMPH_E_VERIFY;
     }
   return AMPH_OK;
@@ -1034,7 +1036,8 @@ int amph_base64_decode(amph_ctx* c, const char* in, size_t nchars, uint8_t* out,
                          return amph::launch_b64_decode((const char*)din[0], 16 * cnt,
                                                         (uint8_t*)dout[0], 12 * cnt, ff, lc,
                                                         false);  // batches never end the text
-                       });
+                       },
+                       16);  // the kernel reports a character offset, 16 per unit
   if (st != AMPH_OK && st != AMPH_E_VERIFY) return st;
   unsigned long long tb = amph::kNoFail;
   const size_t tail_out = ob - 12 * units;

@@ -86,6 +86,14 @@ def decode_diffs(mag, neg) -> List[FactorPair]:
     return [FactorPair(signed[2 * k], signed[2 * k + 1]) for k in range(len(signed) // 2)]
 
 
+def _check_partner(m, own):
+    """A partner must open exactly as many FactorPairs as this party did: the
+    reference's recombineDiffs reads every partner's list at each own index
+    (:231-272) and fails inside the open's Try on a short one."""
+    if tuple(m.shape) != tuple(own.shape):
+        raise ValueError("partner opened %d pairs, expected %d" % (m.shape[0], own.shape[0]))
+
+
 class OutputDeliveryService:
     """OutputDeliveryService with Castor and the inter-VCP open injected.
 
@@ -115,7 +123,18 @@ class OutputDeliveryService:
             data = self._tuples(request_id, tuple_type, count)
         except Exception as e:  # Try.of(..).getOrElseThrow :103-107, :178-185
             raise AmphoraServiceException("Failed to retrieve the required Tuples form Castor") from e
-        return _lib.words_view(data, TUPLE_SIZE[tuple_type])
+        try:
+            tuples = _lib.words_view(data, TUPLE_SIZE[tuple_type])
+        except ValueError as e:
+            raise AmphoraServiceException("Castor returned a malformed %s stream" % tuple_type) from e
+        if tuples.shape[0] != count:
+            # the reference indexes tripleShares.get(i) / inputMasks.get(2i+1) and
+            # fails with IndexOutOfBounds on a short list (:121-139, :186-200); the
+            # kernels take one word count and cannot see a short buffer, so the
+            # stream's length is checked before any launch
+            raise AmphoraServiceException("Castor returned %d %s tuples, %d requested"
+                                          % (tuples.shape[0], tuple_type, count))
+        return tuples
 
     def compute_output_delivery_object(self, share, request_id: uuid.UUID) -> OutputDeliveryObject:
         """computeOutputDeliveryObject(SecretShare | byte[], UUID) :75-161."""
@@ -142,6 +161,7 @@ class OutputDeliveryService:
                     p_op, _, m, n = wire.exchange_from_json(self._ctx, body, mag.shape[0])
                     if p_op != op_id:
                         raise ValueError("operation id %s != %s" % (p_op, op_id))
+                    _check_partner(m, mag)
                     mags.append(m)
                     negs.append(n)
             except Exception as e:
@@ -151,12 +171,13 @@ class OutputDeliveryService:
             self.last_exchange_object = xo
             try:
                 partners = self._exchange(xo)
+                for lst in partners:  # recombineDiffs runs inside the same Try (:205-219)
+                    m, n = encode_diffs(lst)
+                    _check_partner(m, mag)
+                    mags.append(m)
+                    negs.append(n)
             except Exception as e:
                 raise AmphoraServiceException("Failed to open values for operation #%s" % op_id) from e
-            for lst in partners:
-                m, n = encode_diffs(lst)
-                mags.append(m)
-                negs.append(n)
         opened = self._ctx.open_diffs(mags, negs)
         w, u = self._ctx.odo_post(opened, triples, self.player_id == 0)
         return OutputDeliveryObject(y.tobytes(), r.tobytes(), v.tobytes(), w.tobytes(), u.tobytes())

@@ -11,8 +11,9 @@ base64-coded on the GPU (amph_base64_*).
   {"secretId", "data": [{"value": base64(16 bytes)}, ...], "tags"}; each word
   is coded on its own (24 chars), the records are framed with numpy.
 
-Large payloads: the base64 spans are located by key with str.find (no JSON
-tree is built for them); only the small remainder goes through json.loads.
+Large payloads: the base64 spans are located by a structural walk of the
+outermost object that skips strings whole (no JSON tree is built for them);
+only the small remainder goes through json.loads.
 """
 from __future__ import annotations
 
@@ -69,32 +70,77 @@ def odo_to_json(ctx: _lib.Context, odo: OutputDeliveryObject) -> str:
     return "{" + ",".join('"%s":"%s"' % (k, v) for k, v in zip(ODO_FIELDS, b64)) + "}"
 
 
-def _extract(text: str, key: str) -> Tuple[str, int, int]:
-    """Locate "key" : "<value>" and return (value, start, end) of the quoted span."""
-    pat = '"%s"' % key
-    i = text.find(pat)
-    if i < 0:
+_SIGNIFICANT = re.compile(r'["{}\[\]]')
+
+
+def _string_end(text: str, j: int) -> int:
+    """Index of the quote closing the JSON string that opens at text[j]."""
+    k = j + 1
+    while True:
+        k = text.find('"', k)
+        if k < 0:
+            raise ValueError("malformed JSON: unterminated string")
+        b = k - 1
+        while text[b] == "\\":
+            b -= 1
+        if (k - 1 - b) % 2 == 0:  # an even run of backslashes: the quote is not escaped
+            return k
+        k += 1
+
+
+def _top_level_members(text: str):
+    """{key: (key_start, value_start)} of the outermost object's members.
+
+    Only the structure is walked: strings are skipped whole with str.find (the
+    base64 values hold no quotes), so a 100 MB member costs a few calls, and a
+    key nested deeper -- e.g. a tag whose key or value is "rShares" -- is not
+    taken for a member of the object itself."""
+    members, depth, pos = {}, 0, 0
+    while True:
+        m = _SIGNIFICANT.search(text, pos)
+        if m is None:
+            break
+        c, i = m.group(), m.start()
+        if c == '"':
+            e = _string_end(text, i)
+            if depth == 1:
+                j = e + 1
+                while j < len(text) and text[j] in " \t\r\n":
+                    j += 1
+                if j < len(text) and text[j] == ":":
+                    members.setdefault(text[i + 1:e], (i, j + 1))
+            pos = e + 1
+        elif c in "{[":
+            depth += 1
+            pos = i + 1
+        else:
+            depth -= 1
+            pos = i + 1
+            if depth == 0:
+                break
+    return members
+
+
+def _extract(text: str, members, key: str) -> Tuple[str, int, int]:
+    """The string value of top-level member `key`: (value, member start, end)."""
+    if key not in members:
         return None, -1, -1
-    j = i + len(pat)
-    while text[j] in " \t\r\n":
-        j += 1
-    if text[j] != ":":
-        raise ValueError("malformed JSON near %s" % key)
-    j += 1
-    while text[j] in " \t\r\n":
+    i, j = members[key]
+    while j < len(text) and text[j] in " \t\r\n":
         j += 1
     if text.startswith("null", j):
         return None, i, j + 4
-    if text[j] != '"':
+    if j >= len(text) or text[j] != '"':
         raise ValueError("field %s is not a string" % key)
-    k = text.find('"', j + 1)
+    k = _string_end(text, j)
     return text[j + 1:k], i, k + 1
 
 
 def _odo_from_text(ctx: _lib.Context, text: str):
     vals, spans = [], []
+    members = _top_level_members(text)
     for k in ODO_FIELDS:
-        v, s, e = _extract(text, k)
+        v, s, e = _extract(text, members, k)
         if v is None:
             # Lombok @NonNull through Jackson's ValueInstantiationException
             raise IllegalArgumentException("%s is marked non-null but is null" % k)

@@ -125,7 +125,7 @@ def scatter_mode(a, A, torch, dist, ctx, rank, world):
     full_in = None
     if rank == 0:
         _, mb, _ = ctx.synth_odos(seed=21, n=n, words=W)
-        _, sb, _ = ctx.synth_odos(seed=22, n=n, words=W)
+        _, sb, splain = ctx.synth_odos(seed=22, n=n, words=W, with_plain=True)
         sec = ctx.synth_words(seed=23, count=W)
         full_in = [mb[k, j] for k in range(5) for j in range(n)] + \
                   [sb[k, j] for k in range(5) for j in range(n)] + [sec]
@@ -134,6 +134,8 @@ def scatter_mode(a, A, torch, dist, ctx, rank, world):
     flags = A._lib.AMPH_F_DEVICE | A._lib.AMPH_F_ACCUMULATE
     import ctypes as C
     ffp = [C.cast(C.c_void_p(ff.data_ptr() + 8 * i), C.POINTER(C.c_int64)) for i in range(2)]
+
+    last = {}
 
     def step():
         if coll:
@@ -154,9 +156,11 @@ def scatter_mode(a, A, torch, dist, ctx, rank, world):
                                                 stream) == 0
         if coll:
             gather_words(masked, W, 16)
-            gather_words(ys, W, 16)
+            last["ys"] = gather_words(ys, W, 16)
             v = ff.min().view(1).clone()
             dist.all_reduce(v, op=dist.ReduceOp.MIN)
+        else:
+            last["ys"] = ys
 
     for _ in range(a.warmup):
         step()
@@ -179,6 +183,8 @@ def scatter_mode(a, A, torch, dist, ctx, rank, world):
         ok = int(fl.item()) == NO_FAIL
     else:
         ok = int(ff.min().item()) == NO_FAIL
+    if rank == 0:  # the gathered canonical secrets are the generated ones
+        ok = ok and bool(torch.equal(last["ys"], splain))
     if rank == 0:
         emit({"metric": "secret words/s share+recombine incl. RCCL scatter/gather from one GPU",
               "value": W * a.steps / el, "unit": "words/s", "n_gpus": world,
@@ -203,9 +209,10 @@ def host_mode(a, A, torch, ctx):
     _, mb, _ = gen.synth_odos(seed=11, n=n, words=W)
     mask_h = mb.cpu().numpy()
     del mb
-    _, sb, _ = gen.synth_odos(seed=12, n=n, words=W)
+    _, sb, splain = gen.synth_odos(seed=12, n=n, words=W, with_plain=True)
     share_h = sb.cpu().numpy()
-    del sb
+    plain_h = splain.cpu().numpy()
+    del sb, splain
     sec_h = gen.synth_words(seed=13, count=W).cpu().numpy()
     torch.cuda.empty_cache()
     mask_odos = [tuple(mask_h[k, j] for k in range(5)) for j in range(n)]
@@ -229,6 +236,7 @@ def host_mode(a, A, torch, ctx):
         _, f2 = ctx.recombine_verify(share_odos, out=ys_h)
         ok &= f1 == -1 and f2 == -1
     el = time.perf_counter() - t0
+    ok &= bool(np.array_equal(ys_h, plain_h))  # outputs, not only the verdicts
     hbytes = (kbytes("k_mask", n) + kbytes("k_rv", n)) * W
     line = {"metric": "secret words/s host-memory share+recombine (PCIe-inclusive)",
             "value": W * a.steps / el, "unit": "words/s", "n_gpus": ctx.device_count, "steps": a.steps,
@@ -276,6 +284,44 @@ def cpu_baseline(n: int, budget_s: float):
                       "share ODOs), OpenMP %d threads" % (Ws, done // Ws, el, n, threads)}
 
 
+def check_outputs(ctx, lib, torch, C, stream, flags, n, W, secrets, masked, ys, mplain, splain,
+                  share_arr, share_odos, prime, sample=4096):
+    """Output checks of the last timed step, independent of the kernels:
+
+    * K_RV's canonical secrets equal the secrets the share ODOs were generated
+      from (every word, on the device);
+    * K_MASK's masked words equal toGfp((s - m) mod p) for a sample of words,
+      recomputed here with Python integers from the plain secrets s and the
+      plain input masks m (SecretShareUtil.maskInput, SecretShareUtil.java:65-68);
+    * a MAC fault injected into one share word (party 1's w at W // 3) is
+      reported at exactly that index, and the word is restored afterwards."""
+    torch.cuda.synchronize()
+    out = {"secrets_match": bool(torch.equal(ys, splain))}
+    idx = torch.unique(torch.randint(0, W, (min(sample, W),), generator=torch.Generator().manual_seed(7)))
+    s_h = secrets[idx.cuda()].cpu().numpy()
+    m_h = mplain[idx.cuda()].cpu().numpy()
+    got = masked[idx.cuda()].cpu().numpy()
+    R = (1 << 128) % prime
+    good = True
+    for k in range(len(idx)):
+        s_i = int.from_bytes(s_h[k].tobytes(), "little")
+        m_i = int.from_bytes(m_h[k].tobytes(), "little")
+        exp = (((s_i - m_i) % prime) * R % prime).to_bytes(16, "little")
+        good &= exp == got[k].tobytes()
+    out["masked_sample_match"] = bool(good)
+    fi = W // 3
+    wf = share_odos[1 if n > 1 else 0][3]
+    wf[fi, 0] ^= 1
+    ff = torch.full((1,), NO_FAIL, dtype=torch.int64, device="cuda")
+    tmp = torch.empty_like(ys)
+    st = lib.lib.amph_recombine_verify(ctx._h, share_arr, n, tmp.data_ptr(),
+                                       C.cast(C.c_void_p(ff.data_ptr()), C.POINTER(C.c_int64)),
+                                       flags, stream)
+    wf[fi, 0] ^= 1
+    out["fault_detected"] = st == 0 and int(ff.item()) == fi
+    return out
+
+
 def main():
     a = parse()
     _claim_stdout()
@@ -307,8 +353,8 @@ def main():
             dist.destroy_process_group()
         return
     W, n = a.words, a.parties
-    mask_odos, mbuf, _ = ctx.synth_odos(seed=1000 + rank, n=n, words=W)
-    share_odos, sbuf, _ = ctx.synth_odos(seed=2000 + rank, n=n, words=W)
+    mask_odos, mbuf, mplain = ctx.synth_odos(seed=1000 + rank, n=n, words=W, with_plain=True)
+    share_odos, sbuf, splain = ctx.synth_odos(seed=2000 + rank, n=n, words=W, with_plain=True)
     secrets = ctx.synth_words(seed=3000 + rank, count=W)
     torch.cuda.synchronize()
 
@@ -393,6 +439,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, t_mask, t_rv = t.tolist()
     ok = bool((verdicts == NO_FAIL).all().item())
+    # After the timed region: the outputs themselves are checked, not only the
+    # absence of a MAC failure (a kernel that flags nothing and writes wrong
+    # words must not report verified).
+    checks = check_outputs(ctx, lib, torch, C, stream, flags, n, W, secrets, masked, ys, mplain, splain,
+                           share_arr, share_odos, TEST_PRIME)
+    checks["honest_verdicts"] = ok
+    if distributed:
+        cv = torch.tensor([int(all(checks.values()))], dtype=torch.int64, device="cuda")
+        dist.all_reduce(cv, op=dist.ReduceOp.MIN)
+        checks["all_ranks"] = bool(cv.item())
+    ok = all(checks.values())
 
     if rank == 0:
         ms = el * 1000.0 / a.steps
@@ -419,6 +476,7 @@ def main():
                                    % (config_name(W, n), W, n),
                        "words_per_gpu": W, "parties": n, "parallelism": "dp%d" % world},
             "verified": ok,
+            "verify_checks": checks,
             "kernels_ms": {k: round(v, 5) for k, v in kern.items()},
             "kernel_timing": ("HIP events (hipEventDisableSystemFence) %s on the launch stream: "
                               "%d launches of each kernel spread over the %d timed steps"
@@ -439,7 +497,7 @@ def main():
         dist.destroy_process_group()
     if not ok:
         bad = (verdicts != NO_FAIL).any(dim=1).nonzero().flatten().tolist()
-        sys.exit("verification failed on honest synthetic data at steps %r" % bad[:10])
+        sys.exit("verification failed: checks %r, MAC failures at steps %r" % (checks, bad[:10]))
 
 
 if __name__ == "__main__":

@@ -265,3 +265,83 @@ def test_recombine_object(client_util):
     assert client_util.recombine_object([]) == []
     one = SPDZ.to_gfp(5) + b"\x01\x02"
     assert client_util.recombine_object([one, SPDZ.to_gfp(7) + b"\x00\x00"]) == [12]
+
+
+def test_create_secret_more_secrets_than_masks(A, client_util):
+    """More secret words than masks: the mask ODOs are verified first
+    (verifyOutputDeliveryObjects, DefaultAmphoraClient.java:153), so tampered
+    masks raise IntegrityVerificationException; honest ones the index error of
+    inputMasks.get(i) (:155-157)."""
+    from amphora_amd.client import create_masked_input
+    rng = random.Random(8)
+    masks = [rng.randrange(P) for _ in range(10)]
+    f = _odos_for(rng, masks)
+    secret = A.Secret.of([], list(range(11)))
+    with pytest.raises(IndexError):
+        create_masked_input(client_util, secret, [A.OutputDeliveryObject(*x) for x in f])
+    w1 = bytearray(f[1][3])
+    w1[16 * 4] ^= 1
+    f[1][3] = bytes(w1)
+    with pytest.raises(A.IntegrityVerificationException, match="^Verification of secret has failed"):
+        create_masked_input(client_util, secret, [A.OutputDeliveryObject(*x) for x in f])
+
+
+@pytest.mark.parametrize("short", ["masks", "triples"])
+def test_short_castor_stream(A, ctx, kat, short):
+    """A Castor download with fewer tuples than requested is rejected before
+    any kernel reads past it (the reference fails on the missing index)."""
+    from amphora_amd.service import INPUT_MASK_GFP
+    svc, req, _ = _kat2_service(A, ctx, kat)
+    inner = svc._tuples
+
+    def castor(rid, ttype, count):
+        data = inner(rid, ttype, count)
+        cut = (ttype == INPUT_MASK_GFP) == (short == "masks")
+        return data[: -(32 if ttype == INPUT_MASK_GFP else 96)] if cut else data
+
+    svc._tuples = castor
+    k = kat["kat2"]
+    share = A.SecretShare(None, b"".join(SPDZ.to_gfp(v) + SPDZ.to_gfp(0) for v in k["secret_values"]))
+    with pytest.raises(A.AmphoraServiceException, match="tuples, 4 requested"):
+        svc.compute_output_delivery_object(share, req)
+
+
+@pytest.mark.parametrize("fmt", ["objects", "json"])
+def test_short_partner_list(A, ctx, kat, fmt):
+    """A partner that opens fewer FactorPairs than this party fails the open
+    (recombineDiffs inside the open's Try, OutputDeliveryService.java:205-219)."""
+    from amphora_amd.service import OutputDeliveryService
+    k = kat["kat2"]
+    svc0, req, _ = _kat2_service(A, ctx, kat)
+    pairs = k["partner_diffs"][:-1]
+    if fmt == "json":
+        def exchange(body):
+            return [json.dumps({"operationId": k["expected_operation_id"], "playerId": 1,
+                                "interimValues": [{"a": a, "b": b} for a, b in pairs]}).encode()]
+    else:
+        def exchange(xo):
+            return [[A.FactorPair(a, b) for a, b in pairs]]
+    svc = OutputDeliveryService(ctx, 0, svc0._tuples, exchange, exchange_format=fmt)
+    share = A.SecretShare(None, b"".join(SPDZ.to_gfp(v) + SPDZ.to_gfp(0) for v in k["secret_values"]))
+    with pytest.raises(A.AmphoraServiceException, match="^Failed to open values for operation #"):
+        svc.compute_output_delivery_object(share, req)
+
+
+def test_native_length_checks(A, ctx):
+    """The ctypes layer checks buffer lengths the C entry points cannot see."""
+    import numpy as np
+    from amphora_amd._lib import AmphoraNativeError
+    z = lambda n, w=16: np.zeros((n, w), np.uint8)  # noqa: E731
+    with pytest.raises(AmphoraNativeError, match="input-mask tuples"):
+        ctx.odo_pre(z(4, 32), 32, z(7, 32), z(8, 96))
+    with pytest.raises(AmphoraNativeError, match="multiplication triples"):
+        ctx.odo_pre(z(4, 32), 32, z(8, 32), z(7, 96))
+    mag, neg = np.zeros((8, 2, 16), np.uint8), np.zeros((8, 2), np.uint8)
+    with pytest.raises(AmphoraNativeError, match="differ in length"):
+        ctx.open_diffs([mag, mag[:7]], [neg, neg[:7]])
+    with pytest.raises(AmphoraNativeError, match="do not match"):
+        ctx.odo_post(mag[:6], z(8, 96), True)
+    with pytest.raises(AmphoraNativeError, match="inputMasks"):
+        ctx.convert_share(z(5), z(4, 32), 1, False)
+    with pytest.raises(AmphoraNativeError, match="same length"):
+        ctx.recombine_verify([(z(4), z(4), z(3), z(4), z(4))])

@@ -430,6 +430,34 @@ def test_base64_padding_only_at_text_end(ctx):
         ctx.set_batch_words(4 << 20)
 
 
+@pytest.mark.parametrize("devices", [None, [0, 0, 0]])
+def test_base64_bad_index_in_later_batches(ctx, devices):
+    """The reported index of an illegal character is a character offset into
+    the whole text, whichever host batch (16 characters per batch unit) or
+    device shard it falls in."""
+    import amphora_amd as A
+    c = ctx if devices is None else A.Context(P, R, RINV, devices=devices)
+    raw = np.random.default_rng(11).integers(0, 256, 3 * 200_000, dtype=np.uint8).tobytes()
+    good = base64.b64encode(raw)
+    c.set_batch_words(4096)  # 65 536 characters per batch
+    try:
+        for where in (16 * 4096 + 5, 2 * 16 * 4096 + 16 * 100 + 7, 5 * 16 * 4096, len(good) - 9,
+                      len(good) // 3 + 1, 2 * len(good) // 3 + 3):
+            bad = bytearray(good)
+            bad[where] = ord("*")
+            with pytest.raises(ValueError, match="index %d$" % where):
+                c.base64_decode(bytes(bad))
+        # two bad characters: the smaller index wins across batches
+        bad = bytearray(good)
+        bad[3 * 16 * 4096 + 1] = ord("!")
+        bad[16 * 4096 + 2] = ord("!")
+        with pytest.raises(ValueError, match="index %d$" % (16 * 4096 + 2)):
+            c.base64_decode(bytes(bad))
+        assert c.base64_decode(good) == raw
+    finally:
+        c.set_batch_words(4 << 20)
+
+
 @pytest.mark.parametrize("off", [0, 1, 4, 8])
 def test_base64_device_alignment(ctx, off):
     """Bulk (LDS-staged) and per-lane kernels agree for aligned and
@@ -448,3 +476,18 @@ def test_base64_device_alignment(ctx, off):
     e2[off + 50_001] = ord("?")
     _, bad = ctx.base64_decode(e2[off:off + len(exp)])
     assert int(bad.item()) == 50_001
+
+
+def test_vss_json_tags_named_like_fields(ctx):
+    """Tags whose keys or values are the ODO member names (they come before
+    the members in the document) do not shadow the members."""
+    import amphora_amd as A
+    from amphora_amd import wire
+    odo = A.OutputDeliveryObject(b"s" * 32, b"r" * 32, b"v" * 32, b"w" * 32, b"u" * 32)
+    sid = uuid.UUID("80fbba1b-3da8-4b1e-8a2c-cebd65229fad")
+    tags = [{"key": "rShares", "value": "secretShares"}, {"key": "uShares", "value": 'say "wShares"'}]
+    for pretty in (True, False):
+        text = wire.vss_to_json(ctx, sid, tags, odo, pretty=pretty)
+        sid2, tags2, odo2 = wire.vss_from_json(ctx, text)
+        assert sid2 == sid and odo2 == odo
+        assert [(t["key"], t["value"]) for t in tags2] == [(t["key"], t["value"]) for t in tags]
