@@ -328,7 +328,7 @@ def main():
     import torch
     import torch.distributed as dist
     import amphora_amd as A
-    from oracle.amphora_oracle import TEST_PRIME, TEST_R, TEST_RINV  # constants only
+    from amphora_amd.spdz import TEST_PRIME, TEST_R, TEST_RINV
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -9,7 +9,6 @@ three shares) with Python ints, one stream per party, cached per
 import random
 import threading
 
-from oracle.amphora_oracle import MpSpdzIntegrationUtils
 
 INPUT_MASK_GFP = "INPUT_MASK_GFP"
 MULTIPLICATION_TRIPLE_GFP = "MULTIPLICATION_TRIPLE_GFP"
@@ -17,8 +16,7 @@ MULTIPLICATION_TRIPLE_GFP = "MULTIPLICATION_TRIPLE_GFP"
 
 class FakeCastor:
     def __init__(self, prime, r, r_inv, mac_keys, seed=0):
-        self.p = prime
-        self.spdz = MpSpdzIntegrationUtils(prime, r, r_inv)
+        self.p, self.r = prime, r
         self.mac_keys = list(mac_keys)
         self.alpha = sum(mac_keys) % prime
         self.n = len(mac_keys)
@@ -26,6 +24,11 @@ class FakeCastor:
         self.cache = {}
         self.calls = []
         self._lock = threading.Lock()  # parties call concurrently
+
+    def to_gfp(self, x):
+        """Castor's wire word: Montgomery form x*r mod p, 16 bytes little-endian
+        (the assumed mp-spdz-integration encoding)."""
+        return (x * self.r % self.p).to_bytes(16, "little")
 
     def _share(self, x):
         sh = [self.rng.randrange(self.p) for _ in range(self.n - 1)]
@@ -45,7 +48,7 @@ class FakeCastor:
         key = (request_id, ttype)
         if key not in self.cache:
             streams = [bytearray() for _ in range(self.n)]
-            g = self.spdz.to_gfp
+            g = self.to_gfp
             for _ in range(count):
                 if ttype == INPUT_MASK_GFP:
                     parts = [self._auth_share(self.rng.randrange(self.p))]

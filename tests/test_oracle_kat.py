@@ -248,3 +248,10 @@ def test_c_oracle_vs_python_random():
     po = [O.OutputDeliveryObject(*[buf[k, j].tobytes() for k in range(5)]) for j in range(3)]
     assert O.verify_output_delivery_objects(util, po) == [
         int.from_bytes(y[i].tobytes(), "little") for i in range(300)]
+
+
+def test_package_field_constants_match_oracle():
+    """bench.py and the tools take the field from amphora_amd.spdz, never
+    from oracle/: both restate the same reference configuration."""
+    from amphora_amd import spdz
+    assert (spdz.TEST_PRIME, spdz.TEST_R, spdz.TEST_RINV) == (O.TEST_PRIME, O.TEST_R, O.TEST_RINV)

@@ -28,9 +28,9 @@ def main():
     a = ap.parse_args()
     import amphora_amd as A
     from amphora_amd.loopback import AmphoraParty, ExchangeHub, LoopbackAmphoraClient
-    from oracle import amphora_oracle as O
+    from amphora_amd.spdz import TEST_PRIME, TEST_R, TEST_RINV
     from tests.loopback_dealer import FakeCastor
-    P, R, RINV = O.TEST_PRIME, O.TEST_R, O.TEST_RINV
+    P, R, RINV = TEST_PRIME, TEST_R, TEST_RINV
     rng = random.Random(1)
     keys = [rng.randrange(P) for _ in range(a.parties)]
     castor = FakeCastor(P, R, RINV, keys, 1)

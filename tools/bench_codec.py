@@ -8,7 +8,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 import amphora_amd as A  # noqa: E402
-from oracle.amphora_oracle import TEST_PRIME, TEST_R, TEST_RINV  # noqa: E402
+from amphora_amd.spdz import TEST_PRIME, TEST_R, TEST_RINV  # noqa: E402
 
 ctx = A.Context(TEST_PRIME, TEST_R, TEST_RINV)
 L = A._lib.lib

@@ -42,7 +42,7 @@ import os, sys  # noqa: E401,E402
 import numpy as np  # noqa: E402
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import amphora_amd as A  # noqa: E402
-from oracle.amphora_oracle import TEST_PRIME, TEST_R, TEST_RINV  # noqa: E402
+from amphora_amd.spdz import TEST_PRIME, TEST_R, TEST_RINV  # noqa: E402
 ctx = A.Context(TEST_PRIME, TEST_R, TEST_RINV)
 a = np.ones(N, np.uint8)
 ctx.host_register(a)
