@@ -80,6 +80,7 @@ def _load():
     L.amph_odo_pre.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp, u32, vp]
     L.amph_open_diffs.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), i32, sz, vp, u32, vp]
     L.amph_odo_post.argtypes = [vp, vp, vp, sz, i32, vp, vp, u32, vp]
+    L.amph_open_post.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), i32, vp, sz, i32, vp, vp, u32, vp]
     L.amph_host_register.argtypes = [vp, vp, sz]
     L.amph_host_unregister.argtypes = [vp, vp]
     L.amph_time_next_launch.argtypes = [vp, vp]
@@ -107,7 +108,7 @@ EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count",
             "amph_last_error", "amph_version", "amph_recombine_verify", "amph_mask_input",
             "amph_recombine", "amph_verify", "amph_verify_message", "amph_mask_words",
             "amph_to_gfp", "amph_from_gfp", "amph_convert_share", "amph_odo_pre",
-            "amph_open_diffs", "amph_odo_post", "amph_synth_odos", "amph_synth_words",
+            "amph_open_diffs", "amph_odo_post", "amph_open_post", "amph_synth_odos", "amph_synth_words",
             "amph_host_register", "amph_host_unregister", "amph_time_next_launch",
             "amph_timing_event_create", "amph_timing_event_destroy", "amph_timing_event_record",
             "amph_timing_event_elapsed_ms", "amph_base64_encode", "amph_base64_decode",
@@ -393,6 +394,28 @@ class Context:
         w, u = self._empty(tr, (W, 16)), self._empty(tr, (W, 16))
         self._check(lib.amph_odo_post(self._h, _ptr(op), _ptr(tr), W, int(is_player0), _ptr(w),
                                       _ptr(u), flags, stream))
+        return w, u
+
+    def open_post(self, mags, negs, triples96, is_player0: bool):
+        """open_diffs + odo_post in one launch (amph_open_post): every party's
+        signed diffs + the triples -> (w, u); the opened values stay on chip."""
+        ms = [m if _is_dev(m) else np.ascontiguousarray(m, np.uint8) for m in mags]
+        ns = [n if _is_dev(n) else np.ascontiguousarray(n, np.uint8) for n in negs]
+        tr = words_view(triples96, 96)
+        _need(len(ms) == len(ns) and len(ms) >= 1, "one (mag, neg) pair per party")
+        n_pairs = tr.shape[0]
+        _need(n_pairs % 2 == 0, "triples must be 2 per word")
+        for m, n in zip(ms, ns):
+            _need(tuple(m.shape) == (n_pairs, 2, 16) and tuple(n.shape) == (n_pairs, 2),
+                  "party diff lists %s / %s do not match %d triples"
+                  % (tuple(m.shape), tuple(n.shape), n_pairs))
+        flags, stream = self._mode(tr, *ms, *ns)
+        W = n_pairs // 2
+        w, u = self._empty(tr, (W, 16)), self._empty(tr, (W, 16))
+        pm = (C.c_void_p * len(ms))(*[_ptr(x) for x in ms])
+        pn = (C.c_void_p * len(ns))(*[_ptr(x) for x in ns])
+        self._check(lib.amph_open_post(self._h, pm, pn, len(ms), _ptr(tr), W, int(is_player0), _ptr(w),
+                                       _ptr(u), flags, stream))
         return w, u
 
     # -- wire codec (base64 as Jackson writes byte[]) ---------------------------

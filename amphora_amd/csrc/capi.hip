@@ -891,6 +891,46 @@ int amph_odo_post(amph_ctx* c, const uint8_t* opened, const uint8_t* triples, si
                      });
 }
 
+int amph_open_post(amph_ctx* c, const uint8_t* const* mags, const uint8_t* const* negs, int n,
+                   const uint8_t* triples, size_t words, int is_player0, uint8_t* ow, uint8_t* ou,
+                   uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (!mags || !negs || n < 1 || n > AMPH_MAX_PARTIES) return fail(AMPH_E_PARAM, "n_parties must be in [1, 16]");
+  if (words && (!triples || !ow || !ou)) return fail(AMPH_E_PARAM, "null buffer");
+  for (int j = 0; j < n; ++j)
+    if (words && (!mags[j] || !negs[j])) return fail(AMPH_E_PARAM, "null diff array");
+  if (flags & AMPH_F_DEVICE) {
+    for (int j = 0; j < n; ++j)
+      if (int st = check_dev_words({mags[j]})) return st;
+    if (int st = check_dev_words({triples, ow, ou})) return st;
+    HIP_TRY(hipSetDevice(c->device));
+    amph::SignedSet set{};
+    for (int j = 0; j < n; ++j) {
+      set.mag[j] = (const uint4*)mags[j];
+      set.neg[j] = (const uint32_t*)negs[j];
+    }
+    hipError_t e = amph::launch_open_post(set, n, (const uint4*)triples, words, is_player0, (uint4*)ow,
+                                          (uint4*)ou, c->f, cfg(c, (hipStream_t)stream, words));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_open_post");
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  std::vector<HostIn> ins;
+  for (int j = 0; j < n; ++j) ins.push_back({mags[j], 64});
+  for (int j = 0; j < n; ++j) ins.push_back({negs[j], 4});
+  ins.push_back({triples, 192});
+  return run_batched(c, words, ins, {{ow, 16}, {ou, 16}}, false, nullptr,
+                     [&](auto& din, auto& dout, size_t cnt, unsigned long long*,
+                         const amph::LaunchCfg& lc) {
+                       amph::SignedSet set{};
+                       for (int j = 0; j < n; ++j) {
+                         set.mag[j] = din[j];
+                         set.neg[j] = (const uint32_t*)din[n + j];
+                       }
+                       return amph::launch_open_post(set, n, din[2 * n], cnt, is_player0, dout[0],
+                                                     dout[1], c->f, lc);
+                     });
+}
+
 int amph_to_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, uint32_t flags,
                 void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;

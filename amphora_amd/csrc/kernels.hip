@@ -306,6 +306,73 @@ __global__ __launch_bounds__(kPairBlock) void k_odo_post(const uint4* opened,
   st((k & 1 ? ou : ow) + (k >> 1), mod_add(canon<BIG>(c, f), mont_mul(x, r2, f), f));
 }
 
+// recombineDiffs fused into K_ODO_POST (OutputDeliveryService.java:223-228,
+// 231-286): one Beaver pair per lane opens D = sum_j +-d_j and E = sum_j +-e_j
+// from every party's signed diffs and goes straight on to the product share,
+// so the opened values never round-trip through HBM (the two-launch path
+// writes and re-reads 64 B per word: 488 -> 360 B/word at N = 2, 556 -> 428
+// at N = 3).  Each party's diff pair (2 x 16 B) is one 32-B-strided lane
+// access; STAGE_MAG instead brings the workgroup's run of them in through LDS
+// like the triples (tools/ubench/ubench_open_post.hip measures both).
+template <int NP, bool BIG, bool STAGE_MAG>
+__global__ __launch_bounds__(kPairBlock) void k_open_post(SignedSet d, int n, const uint4* triples,
+                                                         size_t pairs, int p0, uint4* ow, uint4* ou,
+                                                         Fp f) {
+  constexpr int kMagSlots = STAGE_MAG ? (NP > 0 ? NP : 1) * kPairBlock * 3 : 0;
+  __shared__ uint4 lds[kPairBlock * 7 + kMagSlots];
+  uint4* tri = lds;
+  const size_t k0 = (size_t)blockIdx.x * kPairBlock;
+  const size_t k = k0 + threadIdx.x;
+  const size_t nblk = min((size_t)kPairBlock, pairs - k0);
+  stage_tuples<6, kPairBlock>(tri, triples + 6 * k0, nblk);
+  W4 D = {}, E = {};
+  if constexpr (NP > 0) {
+    uint4 md[NP], me[NP];
+    uint32_t sg[NP];
+    if constexpr (STAGE_MAG) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j)
+        stage_tuples<2, kPairBlock>(lds + kPairBlock * 7 + j * kPairBlock * 3, d.mag[j] + 2 * k0, nblk);
+    }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      if constexpr (!STAGE_MAG) {
+        md[j] = k < pairs ? ld(d.mag[j] + 2 * k) : make_uint4(0, 0, 0, 0);
+        me[j] = k < pairs ? ld(d.mag[j] + 2 * k + 1) : make_uint4(0, 0, 0, 0);
+      }
+      sg[j] = k < pairs ? reinterpret_cast<const uint16_t*>(d.neg[j])[k] : 0;
+    }
+    __syncthreads();
+    if (k >= pairs) return;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      if constexpr (STAGE_MAG) {
+        md[j] = lds[kPairBlock * 7 + j * kPairBlock * 3 + 3 * threadIdx.x];
+        me[j] = lds[kPairBlock * 7 + j * kPairBlock * 3 + 3 * threadIdx.x + 1];
+      }
+      const W4 x = canon<BIG>(w4(md[j]), f), y = canon<BIG>(w4(me[j]), f);
+      D = (sg[j] & 0xFF) ? mod_sub(D, x, f) : mod_add(D, x, f);
+      E = (sg[j] >> 8) ? mod_sub(E, y, f) : mod_add(E, y, f);
+    }
+  } else {
+    __syncthreads();
+    if (k >= pairs) return;
+    for (int j = 0; j < n; ++j) {
+      const uint32_t s = reinterpret_cast<const uint16_t*>(d.neg[j])[k];
+      const W4 x = canon<BIG>(w4(ld(d.mag[j] + 2 * k)), f), y = canon<BIG>(w4(ld(d.mag[j] + 2 * k + 1)), f);
+      D = (s & 0xFF) ? mod_sub(D, x, f) : mod_add(D, x, f);
+      E = (s >> 8) ? mod_sub(E, y, f) : mod_add(E, y, f);
+    }
+  }
+  // K_ODO_POST on the opened (canonical) D, E
+  const W4 a = w4(tri[threadIdx.x * 7]), b = w4(tri[threadIdx.x * 7 + 2]);
+  const W4 c = w4(tri[threadIdx.x * 7 + 4]);
+  const W4 r2 = r2_word(f);
+  const W4 bb = p0 ? mod_add(canon<BIG>(b, f), mont_mul(E, r2, f), f) : b;
+  const W4 x = dot2_redc(D, bb, E, a, f);
+  st((k & 1 ? ou : ow) + (k >> 1), mod_add(canon<BIG>(c, f), mont_mul(x, r2, f), f));
+}
+
 // MpSpdzIntegrationUtils.toGfp / fromGfp over arrays, and maskInput with
 // canonical masks (SecretShareUtil.java:65-68 word by word).
 template <bool BIG>
@@ -520,6 +587,21 @@ hipError_t launch_odo_post(const uint4* opened, const uint4* triples, size_t wor
   const dim3 g((unsigned)((pairs + kPairBlock - 1) / kPairBlock));
   if (f.big) AMPH_LAUNCH((k_odo_post<true>), g, dim3(kPairBlock), c, opened, triples, pairs, p0, ow, ou, f);
   else AMPH_LAUNCH((k_odo_post<false>), g, dim3(kPairBlock), c, opened, triples, pairs, p0, ow, ou, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_open_post(const SignedSet& d, int n, const uint4* triples, size_t words, int p0,
+                            uint4* ow, uint4* ou, const Fp& f, const LaunchCfg& c, bool stage_mag) {
+  if (words == 0) return hipSuccess;
+  const size_t pairs = 2 * words;
+  const dim3 g((unsigned)((pairs + kPairBlock - 1) / kPairBlock));
+#define L(NP, BIG)                                                                                  \
+  if (stage_mag) AMPH_LAUNCH((k_open_post<NP, BIG, true>), g, dim3(kPairBlock), c, d, n, triples,  \
+                             pairs, p0, ow, ou, f);                                                \
+  else AMPH_LAUNCH((k_open_post<NP, BIG, false>), g, dim3(kPairBlock), c, d, n, triples, pairs, p0, \
+                   ow, ou, f)
+  if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
+#undef L
   return hipGetLastError();
 }
 

@@ -76,6 +76,12 @@ hipError_t launch_odo_post(const uint4* opened, const uint4* triples, size_t wor
                            int is_player0, uint4* out_w, uint4* out_u, const Fp& f,
                            const LaunchCfg& c);
 
+// recombineDiffs + K_ODO_POST in one launch: every party's signed diffs
+// (SignedSet) + triples -> w, u wire words; the opened D, E stay in registers.
+hipError_t launch_open_post(const SignedSet& d, int n, const uint4* triples, size_t words,
+                            int is_player0, uint4* out_w, uint4* out_u, const Fp& f,
+                            const LaunchCfg& c, bool stage_mag = false);
+
 // toGfp / fromGfp over word arrays; maskInput with canonical masks.
 hipError_t launch_to_gfp(const uint4* in, size_t words, uint4* out, const Fp& f, const LaunchCfg& c);
 hipError_t launch_from_gfp(const uint4* in, size_t words, uint4* out, const Fp& f, const LaunchCfg& c);

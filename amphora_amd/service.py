@@ -6,7 +6,8 @@ Mirrors:
       amphora-service/.../calculation/SecretShareUtil.java:30-107     (K_CONV)
 * calculation/OutputDeliveryService.computeOutputDeliveryObject
       amphora-service/.../calculation/OutputDeliveryService.java:57-286
-      local parts: K_ODO_PRE -> exchange -> open (recombineDiffs) -> K_ODO_POST
+      local parts: K_ODO_PRE -> exchange -> open (recombineDiffs) + K_ODO_POST,
+      the last two fused in one launch (amph_open_post)
 * persistence/cache/InputMaskCachingService.getInputMasksAsOutputDeliveryObject
       InputMaskCachingService.java:77-99 (value halves of the mask tuples)
 
@@ -178,8 +179,9 @@ class OutputDeliveryService:
                     negs.append(n)
             except Exception as e:
                 raise AmphoraServiceException("Failed to open values for operation #%s" % op_id) from e
-        opened = self._ctx.open_diffs(mags, negs)
-        w, u = self._ctx.odo_post(opened, triples, self.player_id == 0)
+        # recombineDiffs (:231-272) + multiplySharedSecrets (:274-286) + the w/u
+        # encoding (:147-152), one launch: the opened values stay on chip
+        w, u = self._ctx.open_post(mags, negs, triples, self.player_id == 0)
         return OutputDeliveryObject(y.tobytes(), r.tobytes(), v.tobytes(), w.tobytes(), u.tobytes())
 
     def get_input_masks_as_output_delivery_object(self, request_id: uuid.UUID, count: int):

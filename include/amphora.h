@@ -24,6 +24,8 @@
  *   amph_open_diffs      <- OutputDeliveryService.recombineDiffs :231-272 (the sum)
  *   amph_odo_post        <- OutputDeliveryService.multiplySharedSecrets :274-286
  *                           + w/u encoding :147-152
+ *   amph_open_post       <- recombineDiffs :231-272 + multiplySharedSecrets :274-286
+ *                           + w/u encoding :147-152 (the two calls above, fused)
  *   amph_mask_words      <- SecretShareUtil.maskInput :65-68 (canonical mask given)
  *   amph_to_gfp / amph_from_gfp <- MpSpdzIntegrationUtils.toGfp / fromGfp (call
  *                           sites: client SecretShareUtil.java:56,67; service
@@ -244,6 +246,16 @@ int amph_open_diffs(amph_ctx* ctx, const uint8_t* const* diff_mags,
  * opened: 2*words pairs x 2 canonical LE16 values. */
 int amph_odo_post(amph_ctx* ctx, const uint8_t* opened, const uint8_t* triples, size_t words,
                   int is_player0, uint8_t* out_w, uint8_t* out_u, uint32_t flags, void* stream);
+
+/* recombineDiffs + multiplySharedSecrets + toGfp in one pass (the two calls
+ * above fused: the opened D, E never leave the GPU's registers).  Per pair k:
+ * D, E = sum over n_parties of the signed diffs (amph_open_diffs' inputs),
+ * then out_w / out_u exactly as amph_odo_post.  Same outputs, bit for bit, as
+ * amph_open_diffs followed by amph_odo_post; 360 instead of 488 HBM bytes per
+ * word at 2 parties.  words = n_pairs / 2 = triples / 2. */
+int amph_open_post(amph_ctx* ctx, const uint8_t* const* diff_mags, const uint8_t* const* diff_negs,
+                   int n_parties, const uint8_t* triples, size_t words, int is_player0,
+                   uint8_t* out_w, uint8_t* out_u, uint32_t flags, void* stream);
 
 /* ---- wire codec ----------------------------------
  * Base64 as Jackson writes byte[] (Base64Variants.MIME_NO_LINEFEEDS: standard

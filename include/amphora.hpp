@@ -478,11 +478,9 @@ class OutputDeliveryService {
       mags.push_back(pd.mag.data());
       negs.push_back(pd.neg.data());
     }
-    Bytes opened(64 * W), w(16 * W), u(16 * W);
-    check(amph_open_diffs(ctx_.get(), mags.data(), negs.data(), (int)mags.size(), 2 * W, opened.data(), 0,
-                          nullptr));
-    check(amph_odo_post(ctx_.get(), opened.data(), triples.data(), W, playerId_ == 0, w.data(), u.data(), 0,
-                        nullptr));
+    Bytes w(16 * W), u(16 * W);  // recombineDiffs + multiplySharedSecrets, fused
+    check(amph_open_post(ctx_.get(), mags.data(), negs.data(), (int)mags.size(), triples.data(), W,
+                         playerId_ == 0, w.data(), u.data(), 0, nullptr));
     return OutputDeliveryObject(std::move(y), std::move(r), std::move(v), std::move(w), std::move(u));
   }
 

@@ -102,6 +102,10 @@ def test_golden(golden_dir, ctx, torch, idx, mode):
         w, u = ctx.odo_post(on(d["odo_opened"]), on(d["odo_triples"]), pid == 0)
         assert np.array_equal(back(w), d["odo_w_p%d" % pid])
         assert np.array_equal(back(u), d["odo_u_p%d" % pid])
+        # the fused open + post from the parties' diffs gives the same words
+        w, u = ctx.open_post(mags, negs, on(d["odo_triples"]), pid == 0)
+        assert np.array_equal(back(w), d["odo_w_p%d" % pid])
+        assert np.array_equal(back(u), d["odo_u_p%d" % pid])
 
 
 @pytest.mark.parametrize("n,W", [(1, 777), (2, 100_003), (3, 65_536), (4, 4097), (5, 3000),
@@ -313,6 +317,49 @@ def test_party_kernels_vs_c_oracle(ctx, F):
         w, u = ctx.odo_post(opened, triples, p0)
         ew, eu = F.odo_post(opened, triples, p0)
         assert np.array_equal(w, ew) and np.array_equal(u, eu)
+        w, u = ctx.open_post([mag, pm], [neg, pn], triples, p0)
+        assert np.array_equal(w, ew) and np.array_equal(u, eu)
+
+
+@pytest.mark.parametrize("n,W", [(1, 1), (2, 64), (2, 100_003), (3, 65_537), (4, 4097), (5, 3000),
+                                 (16, 513)])
+def test_open_post_vs_c_oracle(ctx, F, n, W):
+    """amph_open_post (recombineDiffs + multiplySharedSecrets fused) against
+    the C oracle's recombine_diffs + odo_post, every party count path (1-4
+    templated, more at run time), ragged tails of the 128-pair workgroups,
+    sign bytes other than 0/1 (any nonzero byte is negative), host and
+    device buffers."""
+    import torch
+    triples = F.synth_words(seed=40 + n, count=12 * W).reshape(2 * W, 96)
+    mags = [F.synth_words(seed=50 + j, count=4 * W).reshape(2 * W, 2, 16) for j in range(n)]
+    negs = [(F.synth_words(seed=70 + j, count=W)[:, :4].reshape(2 * W, 2) % 3).astype(np.uint8)
+            for j in range(n)]
+    opened = F.recombine_diffs(mags, negs)
+    for p0 in (True, False):
+        ew, eu = F.odo_post(opened, triples, p0)
+        w, u = ctx.open_post(mags, negs, triples, p0)
+        assert np.array_equal(w, ew) and np.array_equal(u, eu), p0
+        dw, du = ctx.open_post([torch.from_numpy(m).cuda() for m in mags],
+                               [torch.from_numpy(x).cuda() for x in negs],
+                               torch.from_numpy(triples).cuda(), p0)
+        torch.cuda.synchronize()
+        assert np.array_equal(dw.cpu().numpy(), ew) and np.array_equal(du.cpu().numpy(), eu), p0
+
+
+def test_open_post_host_batches(ctx, F):
+    """Host-pointer open_post through the batched 3-slot pipeline."""
+    W = 20_011
+    triples = F.synth_words(seed=91, count=12 * W).reshape(2 * W, 96)
+    mags = [F.synth_words(seed=92 + j, count=4 * W).reshape(2 * W, 2, 16) for j in range(3)]
+    negs = [(F.synth_words(seed=95 + j, count=W)[:, :4].reshape(2 * W, 2) & 1).astype(np.uint8)
+            for j in range(3)]
+    ew, eu = F.odo_post(F.recombine_diffs(mags, negs), triples, False)
+    ctx.set_batch_words(4096)
+    try:
+        w, u = ctx.open_post(mags, negs, triples, False)
+    finally:
+        ctx.set_batch_words(4 << 20)
+    assert np.array_equal(w, ew) and np.array_equal(u, eu)
 
 
 def test_codec_and_mask_words(ctx, F):

@@ -93,6 +93,8 @@ def test_odo_kernels_edges(ctx, F, W, n, p0, data):
     w, u = ctx.odo_post(opened, trip, p0 == 1)
     ew, eu = F.odo_post(opened.reshape(2 * W, 32), trip, p0 == 1)
     assert np.array_equal(w, ew) and np.array_equal(u, eu)
+    w, u = ctx.open_post(mags, negs, trip, p0 == 1)
+    assert np.array_equal(w, ew) and np.array_equal(u, eu)
 
 
 @SETTINGS

@@ -1,4 +1,5 @@
-"""Party-side kernels, device-resident: K_CONV, K_ODO_PRE, open, K_ODO_POST.
+"""Party-side kernels, device-resident: K_CONV, K_ODO_PRE, open, K_ODO_POST,
+and the fused open + K_ODO_POST the service runs (k_open_post).
 
     python tools/bench_party.py [--words W] [--parties N] [--reps R]
 
@@ -65,6 +66,8 @@ t, opened = timed(lambda: ctx.open_diffs(mags, negs))
 res["k_open"] = (t, 68 * n + 64)
 t, _ = timed(lambda: ctx.odo_post(opened, triples, True))
 res["k_odo_post"] = (t, 64 + 192 + 32)
+t, _ = timed(lambda: ctx.open_post(mags, negs, triples, True))
+res["k_open_post"] = (t, 68 * n + 192 + 32)  # the product path: open + post fused
 out = {"words": W, "parties": n,
        "kernels": {k: {"ms": round(t, 4), "bytes_per_word": b,
                        "GBps": round(b * W / (t * 1e-3) / 1e9, 1),
