@@ -98,6 +98,7 @@ def _load():
     L.amph_exchange_decode.argtypes = [vp, vp, sz, sz, vp, vp, i64p, u32, vp]
     L.amph_synth_odos.argtypes = [vp, u64, i32, sz, C.POINTER(vp), vp, C.c_int64, i32, vp]
     L.amph_synth_words.argtypes = [vp, u64, sz, vp, vp]
+    L.amph_stream_probe.argtypes = [vp, vp, i32, vp, sz, vp, vp]
     return L
 
 
@@ -113,7 +114,7 @@ EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count",
             "amph_timing_event_create", "amph_timing_event_destroy", "amph_timing_event_record",
             "amph_timing_event_elapsed_ms", "amph_base64_encode", "amph_base64_decode",
             "amph_base64_encode_words", "amph_base64_decode_words", "amph_exchange_max_chars",
-            "amph_exchange_encode", "amph_exchange_decode"]
+            "amph_exchange_encode", "amph_exchange_decode", "amph_stream_probe"]
 
 
 class TimingEvent:

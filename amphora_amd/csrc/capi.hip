@@ -1293,6 +1293,24 @@ int amph_synth_odos(amph_ctx* c, uint64_t seed, int n, size_t words, uint8_t* co
   return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_synth");
 }
 
+int amph_stream_probe(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* secrets, size_t words,
+                      uint8_t* out, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  size_t W;
+  if (int st = odo_words(odos, n, &W)) return st;
+  if (words > W) return fail(AMPH_E_LEN, "more words than the ODO arrays hold");
+  if (words && (!secrets || !out)) return fail(AMPH_E_PARAM, "null secrets/output");
+  if (int st = check_dev_odos(odos, n)) return st;
+  if (int st = check_dev_words({secrets, out})) return st;
+  HIP_TRY(hipSetDevice(c->device));
+  amph::OdoSet set{};
+  for (int k = 0; k < 5; ++k)
+    for (int j = 0; j < n; ++j) set.f[k][j] = (const uint4*)odo_field(odos[j], k);
+  hipError_t e = amph::launch_stream_probe(set, n, words, (const uint4*)secrets, (uint4*)out,
+                                           cfg(c, (hipStream_t)stream, words));
+  return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_stream_probe");
+}
+
 int amph_synth_words(amph_ctx* c, uint64_t seed, size_t count, uint8_t* out, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (count && !out) return fail(AMPH_E_PARAM, "null output");

@@ -458,6 +458,32 @@ __global__ __launch_bounds__(kMaxBlock) void k_synth(OutSet out, int n, size_t w
   }
 }
 
+// Measurement only: K_MASK's exact memory pattern (the same 5N + 1 nontemporal
+// 16-B loads per lane, one 16-B store, same grid) with the field arithmetic
+// replaced by an XOR, so bench.py can time, in the same run and on the same
+// box, what this access pattern achieves at this size with nothing else to do.
+template <int NP>
+__global__ __launch_bounds__(kMaxBlock) void k_stream_probe(OdoSet odo, int n, size_t words,
+                                                        const uint4* secrets, uint4* out) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
+    uint4 x = ld(secrets + i);
+    const int np = NP > 0 ? NP : n;
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+      for (int j = 0; j < (NP > 0 ? NP : kMaxParties); ++j) {
+        if (NP == 0 && j >= np) break;
+        const uint4 v = ld(odo.f[k][j] + i);
+        x.x ^= v.x;
+        x.y ^= v.y;
+        x.z ^= v.z;
+        x.w ^= v.w;
+      }
+    out[i] = x;
+  }
+}
+
 template <bool BIG>
 __global__ __launch_bounds__(kMaxBlock) void k_synth_words(uint4* out, size_t count, uint64_t seed,
                                                        Fp f) {
@@ -637,6 +663,16 @@ hipError_t launch_synth_odos(const OutSet& out, int n, size_t words, uint64_t se
   const unsigned g = grid_for(words, c);
   if (f.big) AMPH_LAUNCH((k_synth<true>), dim3(g), dim3(c.block), c, out, n, words, seed, plain_y, fault, permille, f);
   else AMPH_LAUNCH((k_synth<false>), dim3(g), dim3(c.block), c, out, n, words, seed, plain_y, fault, permille, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_stream_probe(const OdoSet& odo, int n, size_t words, const uint4* secrets,
+                               uint4* out, const LaunchCfg& c) {
+  if (words == 0) return hipSuccess;
+  const unsigned g = grid_for(words, c);
+#define L(NP, BIG) AMPH_LAUNCH((k_stream_probe<NP>), dim3(g), dim3(c.block), c, odo, n, words, secrets, out)
+  AMPH_DISPATCH_NP(n, false, L)
+#undef L
   return hipGetLastError();
 }
 

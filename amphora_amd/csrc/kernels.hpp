@@ -117,5 +117,8 @@ hipError_t launch_synth_odos(const OutSet& out, int n, size_t words, uint64_t se
                              const Fp& f, const LaunchCfg& c);
 hipError_t launch_synth_words(uint4* out, size_t count, uint64_t seed, const Fp& f,
                               const LaunchCfg& c);
+// Measurement only: K_MASK's memory pattern without the arithmetic.
+hipError_t launch_stream_probe(const OdoSet& odo, int n, size_t words, const uint4* secrets,
+                               uint4* out, const LaunchCfg& c);
 
 }  // namespace amph

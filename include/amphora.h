@@ -320,6 +320,14 @@ int amph_synth_odos(amph_ctx* ctx, uint64_t seed, int n_parties, size_t words,
                     int noncanon_permille, void* stream);
 /* Uniform canonical field elements (LE16), device, async on `stream`. */
 int amph_synth_words(amph_ctx* ctx, uint64_t seed, size_t count, uint8_t* out, void* stream);
+/* Measurement only (bench.py): K_MASK's exact memory pattern -- the 5n
+ * ODO word arrays + the secrets read with the same nontemporal 16-B loads,
+ * one 16-B word written per word, same grid -- with the field arithmetic
+ * replaced by an XOR.  Device pointers, async on `stream`; honours
+ * amph_time_next_launch.  Its duration is the bandwidth this access pattern
+ * achieves at this size on this GPU, the practical ceiling for K_MASK. */
+int amph_stream_probe(amph_ctx* ctx, const amph_odo* odos, int n_parties, const uint8_t* secrets,
+                      size_t words, uint8_t* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -501,3 +501,27 @@ def test_device_arrays_must_be_aligned(ctx, torch):
     rec = raw[4:4 + 24 * 100].view(100, 24)  # 4-byte aligned records
     with pytest.raises((A._lib.AmphoraNativeError, ValueError), match="8-byte aligned"):
         ctx.base64_decode_words(rec)
+
+
+def test_stream_probe_pattern(ctx, F):
+    """amph_stream_probe (bench.py's same-pattern ceiling kernel) reads every
+    array K_MASK reads: its output is the XOR of all of them."""
+    import ctypes as C
+    import torch
+    import amphora_amd as A
+    for n in (2, 3, 6):
+        W = 10_007
+        odos, _ = F.synth_odos(seed=300 + n, n=n, W=W)
+        sec = F.synth_words(seed=310 + n, count=W)
+        dodos = [tuple(torch.from_numpy(f).cuda() for f in o) for o in odos]
+        arr, _ = ctx._odo_structs(dodos)
+        ds = torch.from_numpy(sec).cuda()
+        out = torch.empty((W, 16), dtype=torch.uint8, device="cuda")
+        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        assert A._lib.lib.amph_stream_probe(ctx._h, arr, n, ds.data_ptr(), W, out.data_ptr(), stream) == 0
+        exp = sec.copy()
+        for o in odos:
+            for f in o:
+                exp ^= f
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), exp), n
