@@ -99,6 +99,8 @@ def _load():
     L.amph_synth_odos.argtypes = [vp, u64, i32, sz, C.POINTER(vp), vp, C.c_int64, i32, vp]
     L.amph_synth_words.argtypes = [vp, u64, sz, vp, vp]
     L.amph_stream_probe.argtypes = [vp, vp, i32, vp, sz, vp, vp]
+    L.amph_recombine_verify_b64.argtypes = [vp, vp, i32, sz, vp, i64p, i64p, u32, vp]
+    L.amph_mask_input_b64.argtypes = [vp, vp, i32, sz, vp, sz, vp, vp, i64p, i64p, u32, vp]
     return L
 
 
@@ -114,7 +116,8 @@ EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count",
             "amph_timing_event_create", "amph_timing_event_destroy", "amph_timing_event_record",
             "amph_timing_event_elapsed_ms", "amph_base64_encode", "amph_base64_decode",
             "amph_base64_encode_words", "amph_base64_decode_words", "amph_exchange_max_chars",
-            "amph_exchange_encode", "amph_exchange_decode", "amph_stream_probe"]
+            "amph_exchange_encode", "amph_exchange_decode", "amph_stream_probe",
+            "amph_recombine_verify_b64", "amph_mask_input_b64"]
 
 
 class TimingEvent:
@@ -140,6 +143,11 @@ class TimingEvent:
 class _AmphOdo(C.Structure):
     _fields_ = [("secret_shares", C.c_void_p), ("r_shares", C.c_void_p), ("v_shares", C.c_void_p),
                 ("w_shares", C.c_void_p), ("u_shares", C.c_void_p), ("nbytes", C.c_size_t)]
+
+
+class _AmphOdoB64(C.Structure):  # amph_odo_b64: one party's five base64 field texts
+    _fields_ = [("secret_shares", C.c_void_p), ("r_shares", C.c_void_p), ("v_shares", C.c_void_p),
+                ("w_shares", C.c_void_p), ("u_shares", C.c_void_p), ("nchars", C.c_size_t)]
 
 
 def le16(x: int) -> bytes:
@@ -418,6 +426,65 @@ class Context:
         self._check(lib.amph_open_post(self._h, pm, pn, len(ms), _ptr(tr), W, int(is_player0), _ptr(w),
                                        _ptr(u), flags, stream))
         return w, u
+
+    # -- K_RV / K_MASK straight from the base64 wire text ----------------------
+    def _text_structs(self, texts):
+        """texts: per party the five field strings (str / bytes / uint8 arrays,
+        or 16-byte-aligned uint8 device tensors) in ODO order."""
+        arr = (_AmphOdoB64 * len(texts))()
+        keep = []
+        for j, t in enumerate(texts):
+            if len(t) != 5:
+                raise ValueError("five base64 fields per party")
+            fs = []
+            for x in t:
+                if isinstance(x, str):
+                    x = x.encode("ascii", errors="replace")
+                if isinstance(x, (bytes, bytearray, memoryview)):
+                    x = np.frombuffer(bytes(x), np.uint8)
+                elif not _is_dev(x):
+                    x = np.ascontiguousarray(x, np.uint8).reshape(-1)
+                fs.append(x)
+            lens = {(f.numel() if _is_dev(f) else f.size) for f in fs}
+            if len(lens) != 1:
+                raise AmphoraNativeError(AMPH_E_LEN, "The provided shares must be of the same length")
+            keep.extend(fs)
+            arr[j] = _AmphOdoB64(*[_ptr(f) for f in fs], lens.pop())
+        return arr, keep
+
+    def recombine_verify_b64(self, texts, words: int):
+        """amph_recombine_verify_b64: (canonical secrets (W, 16), first_fail,
+        bad_char).  Host: first_fail / bad_char are -1 or indices (a bad
+        character raises ValueError); device: int64[1] tensors."""
+        arr, keep = self._text_structs(texts)
+        flags, stream = self._mode(*keep)
+        out = self._empty(keep[0], (words, 16))
+        ff, ffp = self._ff(keep[0])
+        bad, badp = self._ff(keep[0])
+        st = lib.amph_recombine_verify_b64(self._h, arr, len(texts), words, _ptr(out), ffp, badp, flags, stream)
+        if st == AMPH_E_PARAM and not _is_dev(keep[0]) and self._ff_value(bad) >= 0:
+            raise ValueError(lib.amph_last_error().decode())
+        self._check(st, allow_verify=True)
+        return out, self._ff_value(ff), self._ff_value(bad)
+
+    def mask_input_b64(self, texts, words: int, secrets16, records: bool = True, raw: bool = False):
+        """amph_mask_input_b64: (masked (S, 16) or None, records (S, 24) or
+        None, first_fail, bad_char)."""
+        arr, keep = self._text_structs(texts)
+        sv = words_view(secrets16)
+        flags, stream = self._mode(sv, *keep)
+        S = sv.shape[0]
+        o16 = self._empty(sv, (S, 16)) if raw else None
+        o24 = self._empty(sv, (S, 24)) if records else None
+        ff, ffp = self._ff(sv)
+        bad, badp = self._ff(sv)
+        st = lib.amph_mask_input_b64(self._h, arr, len(texts), words, _ptr(sv), S,
+                                     _ptr(o16) if raw else None, _ptr(o24) if records else None,
+                                     ffp, badp, flags, stream)
+        if st == AMPH_E_PARAM and not _is_dev(sv) and self._ff_value(bad) >= 0:
+            raise ValueError(lib.amph_last_error().decode())
+        self._check(st, allow_verify=True)
+        return o16, o24, self._ff_value(ff), self._ff_value(bad)
 
     # -- wire codec (base64 as Jackson writes byte[]) ---------------------------
     def base64_encode(self, data) -> bytes:

@@ -1,0 +1,116 @@
+// Base64 group coding shared by the wire codec (codec.hip) and the fused
+// wire-format kernels (kernels.hip): Jackson's Base64Variants.MIME_NO_LINEFEEDS
+// alphabet, 4 characters <-> 3 bytes, branch-free SWAR / v_perm table lookups.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace amph {
+
+// 4 base64 chars (little-endian bytes, first char lowest) -> the 24-bit group
+// (first char in the top 6 bits).  inv: bit 7 of byte j set iff char j is
+// not in the alphabet.  Table lookups with v_perm_b32 (8-entry byte tables):
+// class = HI[c >> 4] & LO[c & 15], valid iff nonzero, with the bits
+//   1 '+' '/' (high nibble 2, low B / F)   2 digits (high 3, low 0-9)
+//   4 'A'-'O' 'a'-'o' (high 4 / 6, low 1-15)   8 'P'-'Z' 'p'-'z' (high 5 / 7, low 0-A)
+//   0x10 '/' (low F within high 2);
+// value = c + ROLL[c >> 4] bytewise (carry-free), 3 less for '/'.  ~27 VALU
+// ops per 4 chars (dec6's compare/select chain took ~17 per char).
+__device__ __forceinline__ uint32_t dec4(uint32_t w, uint32_t& inv) {
+  const uint32_t lo = w & 0x0F0F0F0Fu, l7 = lo & 0x07070707u, h7 = (w >> 4) & 0x07070707u;
+  const uint32_t la = __builtin_amdgcn_perm(0x0E0E0E0Eu, 0x0E0E0E0Au, l7);  // LO[0..7]
+  const uint32_t lb = __builtin_amdgcn_perm(0x15040404u, 0x050C0E0Eu, l7);  // LO[8..15]
+  const uint32_t cl = __builtin_amdgcn_perm(lb, la, 0x03020100u | ((lo & 0x08080808u) >> 1));
+  const uint32_t cls = __builtin_amdgcn_perm(0x08040804u, 0x02110000u, h7) & cl;
+  inv = ~(((cls & 0x0F0F0F0Fu) + 0x7F7F7F7Fu) & ~w) & 0x80808080u;
+  const uint32_t roll = __builtin_amdgcn_perm(0xB9B9BFBFu, 0x04130000u, h7);
+  uint32_t v = ((w & 0x7F7F7F7Fu) + (roll & 0x7F7F7F7Fu)) ^ ((w ^ roll) & 0x80808080u);
+  const uint32_t fix = (cls >> 4) & 0x01010101u;
+  v -= fix + (fix << 1);
+  return ((v & 0x3Fu) << 18) | ((v & 0x3F00u) << 4) | ((v >> 10) & 0xFC0u) | (v >> 24);
+}
+
+// group -> its 3 bytes in text order in the low 24 bits
+__device__ __forceinline__ uint32_t group_bytes(uint32_t g) {
+  return __builtin_amdgcn_perm(g, g, 0x0C000102u);
+}
+
+// 24-bit group (first char in the top 6 bits) -> its 4 chars, packed
+// little-endian.  SWAR over the four 6-bit values: idx = (v >= 26) + (v >= 52)
+// + (v >= 62) + (v >= 63) picks the offset to ASCII from a v_perm byte table
+// ('A', 'a' - 26, '0' - 52, '+' - 62, '/' - 63), added carry-free.
+__device__ __forceinline__ uint32_t enc4(uint32_t g) {
+  const uint32_t v = ((g >> 18) & 0x3Fu) | ((g >> 4) & 0x3F00u) | ((g << 10) & 0x3F0000u) |
+                     ((g << 24) & 0x3F000000u);
+  const uint32_t idx = (((v + 0x66666666u) >> 7) & 0x01010101u) + (((v + 0x4C4C4C4Cu) >> 7) & 0x01010101u) +
+                       (((v + 0x42424242u) >> 7) & 0x01010101u) + (((v + 0x41414141u) >> 7) & 0x01010101u);
+  const uint32_t off = __builtin_amdgcn_perm(0x000000F0u, 0xEDFC4741u, idx);
+  return ((v & 0x7F7F7F7Fu) + (off & 0x7F7F7F7Fu)) ^ ((v ^ off) & 0x80808080u);
+}
+
+// 3 bytes (big-endian group) -> 4 chars packed little-endian in a uint32
+__device__ __forceinline__ uint32_t enc_group(uint32_t b0, uint32_t b1, uint32_t b2) {
+  return enc4((b0 << 16) | (b1 << 8) | b2);
+}
+
+
+// 4 base64 chars -> their four 6-bit values (one per byte, same order) and
+// a validity mask (bit 7 of byte j set iff char j is in the alphabet): the
+// table lookups of dec4 without its packing or inverted mask.
+__device__ __forceinline__ uint32_t dec4_values(uint32_t w, uint32_t& valid) {
+  const uint32_t lo = w & 0x0F0F0F0Fu, l7 = lo & 0x07070707u, h7 = (w >> 4) & 0x07070707u;
+  const uint32_t la = __builtin_amdgcn_perm(0x0E0E0E0Eu, 0x0E0E0E0Au, l7);
+  const uint32_t lb = __builtin_amdgcn_perm(0x15040404u, 0x050C0E0Eu, l7);
+  const uint32_t cl = __builtin_amdgcn_perm(lb, la, 0x03020100u | ((lo & 0x08080808u) >> 1));
+  const uint32_t cls = __builtin_amdgcn_perm(0x08040804u, 0x02110000u, h7) & cl;
+  valid = ((cls & 0x0F0F0F0Fu) + 0x7F7F7F7Fu) & ~w;  // bit 7: in the alphabet (and ASCII)
+  const uint32_t roll = __builtin_amdgcn_perm(0xB9B9BFBFu, 0x04130000u, h7);
+  uint32_t v = ((w & 0x7F7F7F7Fu) + (roll & 0x7F7F7F7Fu)) ^ ((w ^ roll) & 0x80808080u);
+  const uint32_t fix = (cls >> 4) & 0x01010101u;
+  return v - (fix + (fix << 1));
+}
+
+// One full 16-character unit (4 groups, no padding) -> its 12 bytes as 3
+// little-endian dwords; returns the offset of the first invalid character in
+// the unit, or 0xFFFFFFFF.  Each group's 24 bits come from two
+// v_dot4_u32_u8 (64 v0 + v1, 64 v2 + v3) and one shift-or, the 12 bytes from
+// three v_perm_b32 straight out of the four groups; validity is one AND per
+// group, the offset is only searched for when some character is bad.
+__device__ __forceinline__ uint32_t dec_unit16(const uint4 v, uint32_t (&o)[3]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t g[4], ok = 0x80808080u, val[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t x = dec4_values(w[q], val[q]);
+    ok &= val[q];
+    g[q] = (__builtin_amdgcn_udot4(x, 0x00000140u, 0u, false) << 12) |
+           __builtin_amdgcn_udot4(x, 0x01400000u, 0u, false);
+  }
+  // bytes in text order: g0[23:16] g0[15:8] g0[7:0] g1[23:16] | g1[15:8] ...
+  o[0] = __builtin_amdgcn_perm(g[1], g[0], 0x06000102u);
+  o[1] = __builtin_amdgcn_perm(g[2], g[1], 0x05060001u);
+  o[2] = __builtin_amdgcn_perm(g[3], g[2], 0x04050600u);
+  if (ok == 0x80808080u) return 0xFFFFFFFFu;
+  uint32_t firstbad = 0xFFFFFFFFu;
+#pragma unroll
+  for (int q = 3; q >= 0; --q) {
+    const uint32_t inv = ~val[q] & 0x80808080u;
+    if (inv) firstbad = 4 * q + (__builtin_ctz(inv) >> 3);
+  }
+  return firstbad;
+}
+
+// A 16-byte word -> its 24-character record (5 full groups, then 1 byte and
+// "=="), as 6 little-endian dwords.
+__device__ __forceinline__ void enc_word24(const uint4 v, uint32_t (&g)[6]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint8_t b[18];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) b[q] = (w[q >> 2] >> (8 * (q & 3))) & 0xFF;
+  b[16] = b[17] = 0;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) g[q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
+  g[5] = (g[5] & 0xFFFFu) | ((uint32_t)'=' << 16) | ((uint32_t)'=' << 24);
+}
+
+}  // namespace amph

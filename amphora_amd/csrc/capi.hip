@@ -1260,6 +1260,177 @@ int amph_exchange_decode(amph_ctx* c, const char* text, size_t len, size_t npair
   return AMPH_OK;
 }
 
+// ---- K_RV / K_MASK from the wire ----------------------------------------------
+namespace {
+const char* const kOdoFieldNames[5] = {"secretShares", "rShares", "vShares", "wShares", "uShares"};
+
+const char* b64_field(const amph_odo_b64& o, int k) {
+  switch (k) {
+    case 0: return o.secret_shares;
+    case 1: return o.r_shares;
+    case 2: return o.v_shares;
+    case 3: return o.w_shares;
+    default: return o.u_shares;
+  }
+}
+
+// Shared checks; *nchars / *pad for `words` 16-byte words.
+int wire_check(const amph_odo_b64* odos, int n, size_t words, size_t* nchars, uint32_t* pad) {
+  if (!odos || n < 1 || n > AMPH_MAX_PARTIES)
+    return fail(AMPH_E_PARAM, "n_parties must be in [1, 16] with a non-null ODO array");
+  const size_t nb = 16 * words;
+  *nchars = 4 * ((nb + 2) / 3);
+  *pad = (uint32_t)((3 - nb % 3) % 3);
+  for (int j = 0; j < n; ++j) {
+    if (odos[j].nchars != *nchars)
+      return fail(AMPH_E_LEN, "party " + std::to_string(j) + ": base64 fields of " +
+                                  std::to_string(odos[j].nchars) + " characters, expected " +
+                                  std::to_string(*nchars) + " for " + std::to_string(words) + " words");
+    for (int k = 0; k < 5 && words; ++k)
+      if (!b64_field(odos[j], k)) return fail(AMPH_E_PARAM, "null ODO field text");
+  }
+  return AMPH_OK;
+}
+
+int wire_bad_message(int64_t bad, size_t nchars) {
+  const size_t o = (size_t)bad / nchars, at = (size_t)bad % nchars;
+  return fail(AMPH_E_PARAM, "Illegal base64 character at index " + std::to_string(at) + " of party " +
+                                std::to_string(o / 5) + "'s " + kOdoFieldNames[o % 5]);
+}
+
+// Host mode: the texts go to the device in one copy each (no batching: the
+// whole call is one launch), outputs come back, verdicts are read.
+struct WireHost {
+  AsyncBuf text, out, out2, words16, flags;
+  amph::TextSet tx{};
+  int stage(const amph_odo_b64* odos, int n, size_t nchars, hipStream_t s) {
+    const size_t stride = (nchars + 15) & ~(size_t)15;
+    HIP_TRY(text.alloc(5 * n * stride, s));
+    for (int j = 0; j < n; ++j)
+      for (int k = 0; k < 5; ++k) {
+        char* d = (char*)text.p + (5 * j + k) * stride;
+        if (nchars) HIP_TRY(hipMemcpyAsync(d, b64_field(odos[j], k), nchars, hipMemcpyHostToDevice, s));
+        tx.t[k][j] = d;
+      }
+    HIP_TRY(flags.alloc(16, s));
+    HIP_TRY(hipMemsetAsync(flags.p, 0x7F, 16, s));
+    return AMPH_OK;
+  }
+};
+}  // namespace
+
+int amph_recombine_verify_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size_t words,
+                              uint8_t* out_secrets, int64_t* first_fail, int64_t* bad_char,
+                              uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  size_t nchars;
+  uint32_t pad;
+  if (int st = wire_check(odos, n, words, &nchars, &pad)) return st;
+  if (words && !out_secrets) return fail(AMPH_E_PARAM, "null output");
+  HIP_TRY(hipSetDevice(c->device));
+  if (flags & AMPH_F_DEVICE) {
+    amph::TextSet tx{};
+    for (int j = 0; j < n; ++j)
+      for (int k = 0; k < 5; ++k) {
+        tx.t[k][j] = b64_field(odos[j], k);
+        if (int st = check_dev_words({tx.t[k][j]})) return st;
+      }
+    if (int st = check_dev_words({out_secrets})) return st;
+    hipStream_t s = (hipStream_t)stream;
+    if (int st = reset_ff_dev(first_fail, flags, s)) return st;
+    if (int st = reset_ff_dev(bad_char, flags, s)) return st;
+    hipError_t e = amph::launch_rv_b64(tx, n, words, nchars, pad, (uint4*)out_secrets,
+                                       (unsigned long long*)first_fail, (unsigned long long*)bad_char,
+                                       c->f, cfg(c, s, words));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_rv_b64");
+  }
+  if (first_fail) *first_fail = -1;
+  if (bad_char) *bad_char = -1;
+  if (words == 0) return AMPH_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipStream_t s;
+  if (int st = host_stream0(c, &s)) return st;
+  WireHost h;
+  if (int st = h.stage(odos, n, nchars, s)) return st;
+  HIP_TRY(h.out.alloc(16 * words, s));
+  unsigned long long* fl = (unsigned long long*)h.flags.p;
+  hipError_t e = amph::launch_rv_b64(h.tx, n, words, nchars, pad, (uint4*)h.out.p, fl, fl + 1, c->f,
+                                     cfg(c, s, words));
+  if (e != hipSuccess) return hip_fail(e, "k_rv_b64");
+  int64_t v[2];
+  HIP_TRY(hipMemcpyAsync(v, fl, 16, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(out_secrets, h.out.p, 16 * words, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (v[1] != (int64_t)AMPH_NO_FAILURE) {
+    if (bad_char) *bad_char = v[1];
+    return wire_bad_message(v[1], nchars);
+  }
+  if (v[0] != (int64_t)AMPH_NO_FAILURE) {
+    if (first_fail) *first_fail = v[0];
+    return AMPH_E_VERIFY;
+  }
+  return AMPH_OK;
+}
+
+int amph_mask_input_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size_t words,
+                        const uint8_t* secrets, size_t n_secrets, uint8_t* out16, char* out24,
+                        int64_t* first_fail, int64_t* bad_char, uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  size_t nchars;
+  uint32_t pad;
+  if (int st = wire_check(odos, n, words, &nchars, &pad)) return st;
+  if (n_secrets > words) return fail(AMPH_E_LEN, "more secret words than verified input masks");
+  if (n_secrets && !secrets) return fail(AMPH_E_PARAM, "null secrets");
+  HIP_TRY(hipSetDevice(c->device));
+  if (flags & AMPH_F_DEVICE) {
+    amph::TextSet tx{};
+    for (int j = 0; j < n; ++j)
+      for (int k = 0; k < 5; ++k) {
+        tx.t[k][j] = b64_field(odos[j], k);
+        if (int st = check_dev_words({tx.t[k][j]})) return st;
+      }
+    if (int st = check_dev_words({secrets, out16, out24})) return st;
+    hipStream_t s = (hipStream_t)stream;
+    if (int st = reset_ff_dev(first_fail, flags, s)) return st;
+    if (int st = reset_ff_dev(bad_char, flags, s)) return st;
+    hipError_t e = amph::launch_mask_b64(tx, n, words, nchars, pad, (const uint4*)secrets, n_secrets,
+                                         (uint4*)out16, out24, (unsigned long long*)first_fail,
+                                         (unsigned long long*)bad_char, c->f, cfg(c, s, words));
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_mask_b64");
+  }
+  if (first_fail) *first_fail = -1;
+  if (bad_char) *bad_char = -1;
+  if (words == 0) return AMPH_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipStream_t s;
+  if (int st = host_stream0(c, &s)) return st;
+  WireHost h;
+  if (int st = h.stage(odos, n, nchars, s)) return st;
+  HIP_TRY(h.words16.alloc(16 * n_secrets, s));
+  if (n_secrets) HIP_TRY(hipMemcpyAsync(h.words16.p, secrets, 16 * n_secrets, hipMemcpyHostToDevice, s));
+  if (out16) HIP_TRY(h.out.alloc(16 * n_secrets, s));
+  if (out24) HIP_TRY(h.out2.alloc(24 * n_secrets, s));
+  unsigned long long* fl = (unsigned long long*)h.flags.p;
+  hipError_t e = amph::launch_mask_b64(h.tx, n, words, nchars, pad, (const uint4*)h.words16.p, n_secrets,
+                                       out16 ? (uint4*)h.out.p : nullptr, out24 ? (char*)h.out2.p : nullptr,
+                                       fl, fl + 1, c->f, cfg(c, s, words));
+  if (e != hipSuccess) return hip_fail(e, "k_mask_b64");
+  int64_t v[2];
+  HIP_TRY(hipMemcpyAsync(v, fl, 16, hipMemcpyDeviceToHost, s));
+  if (out16 && n_secrets) HIP_TRY(hipMemcpyAsync(out16, h.out.p, 16 * n_secrets, hipMemcpyDeviceToHost, s));
+  if (out24 && n_secrets) HIP_TRY(hipMemcpyAsync(out24, h.out2.p, 24 * n_secrets, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (v[1] != (int64_t)AMPH_NO_FAILURE) {
+    if (bad_char) *bad_char = v[1];
+    return wire_bad_message(v[1], nchars);
+  }
+  if (v[0] != (int64_t)AMPH_NO_FAILURE) {
+    if (first_fail) *first_fail = v[0];
+    return AMPH_E_VERIFY;
+  }
+  return AMPH_OK;
+}
+
 int amph_host_register(amph_ctx* c, void* ptr, size_t bytes) {
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (!ptr || !bytes) return fail(AMPH_E_PARAM, "null or empty range");

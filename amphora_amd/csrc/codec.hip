@@ -14,6 +14,7 @@
 #include <hip/hip_ext.h>
 
 #include "kernels.hpp"
+#include "b64.hpp"
 
 namespace amph {
 
@@ -32,52 +33,6 @@ __device__ __forceinline__ uint32_t dec6(uint32_t c) {
   v = c == '+' ? 62u : v;
   v = c == '/' ? 63u : v;
   return v;
-}
-
-// 4 base64 chars (little-endian bytes, first char lowest) -> the 24-bit group
-// (first char in the top 6 bits).  inv: bit 7 of byte j set iff char j is
-// not in the alphabet.  Table lookups with v_perm_b32 (8-entry byte tables):
-// class = HI[c >> 4] & LO[c & 15], valid iff nonzero, with the bits
-//   1 '+' '/' (high nibble 2, low B / F)   2 digits (high 3, low 0-9)
-//   4 'A'-'O' 'a'-'o' (high 4 / 6, low 1-15)   8 'P'-'Z' 'p'-'z' (high 5 / 7, low 0-A)
-//   0x10 '/' (low F within high 2);
-// value = c + ROLL[c >> 4] bytewise (carry-free), 3 less for '/'.  ~27 VALU
-// ops per 4 chars (dec6's compare/select chain took ~17 per char).
-__device__ __forceinline__ uint32_t dec4(uint32_t w, uint32_t& inv) {
-  const uint32_t lo = w & 0x0F0F0F0Fu, l7 = lo & 0x07070707u, h7 = (w >> 4) & 0x07070707u;
-  const uint32_t la = __builtin_amdgcn_perm(0x0E0E0E0Eu, 0x0E0E0E0Au, l7);  // LO[0..7]
-  const uint32_t lb = __builtin_amdgcn_perm(0x15040404u, 0x050C0E0Eu, l7);  // LO[8..15]
-  const uint32_t cl = __builtin_amdgcn_perm(lb, la, 0x03020100u | ((lo & 0x08080808u) >> 1));
-  const uint32_t cls = __builtin_amdgcn_perm(0x08040804u, 0x02110000u, h7) & cl;
-  inv = ~(((cls & 0x0F0F0F0Fu) + 0x7F7F7F7Fu) & ~w) & 0x80808080u;
-  const uint32_t roll = __builtin_amdgcn_perm(0xB9B9BFBFu, 0x04130000u, h7);
-  uint32_t v = ((w & 0x7F7F7F7Fu) + (roll & 0x7F7F7F7Fu)) ^ ((w ^ roll) & 0x80808080u);
-  const uint32_t fix = (cls >> 4) & 0x01010101u;
-  v -= fix + (fix << 1);
-  return ((v & 0x3Fu) << 18) | ((v & 0x3F00u) << 4) | ((v >> 10) & 0xFC0u) | (v >> 24);
-}
-
-// group -> its 3 bytes in text order in the low 24 bits
-__device__ __forceinline__ uint32_t group_bytes(uint32_t g) {
-  return __builtin_amdgcn_perm(g, g, 0x0C000102u);
-}
-
-// 24-bit group (first char in the top 6 bits) -> its 4 chars, packed
-// little-endian.  SWAR over the four 6-bit values: idx = (v >= 26) + (v >= 52)
-// + (v >= 62) + (v >= 63) picks the offset to ASCII from a v_perm byte table
-// ('A', 'a' - 26, '0' - 52, '+' - 62, '/' - 63), added carry-free.
-__device__ __forceinline__ uint32_t enc4(uint32_t g) {
-  const uint32_t v = ((g >> 18) & 0x3Fu) | ((g >> 4) & 0x3F00u) | ((g << 10) & 0x3F0000u) |
-                     ((g << 24) & 0x3F000000u);
-  const uint32_t idx = (((v + 0x66666666u) >> 7) & 0x01010101u) + (((v + 0x4C4C4C4Cu) >> 7) & 0x01010101u) +
-                       (((v + 0x42424242u) >> 7) & 0x01010101u) + (((v + 0x41414141u) >> 7) & 0x01010101u);
-  const uint32_t off = __builtin_amdgcn_perm(0x000000F0u, 0xEDFC4741u, idx);
-  return ((v & 0x7F7F7F7Fu) + (off & 0x7F7F7F7Fu)) ^ ((v ^ off) & 0x80808080u);
-}
-
-// 3 bytes (big-endian group) -> 4 chars packed little-endian in a uint32
-__device__ __forceinline__ uint32_t enc_group(uint32_t b0, uint32_t b1, uint32_t b2) {
-  return enc4((b0 << 16) | (b1 << 8) | b2);
 }
 
 __global__ __launch_bounds__(kMaxBlock) void k_b64_encode(const uint8_t* in, size_t nbytes,

@@ -28,6 +28,10 @@ struct SignedSet {  // per party: diff magnitudes (2 words per pair) + sign word
   const uint32_t* neg[kMaxParties];  // 4 sign bytes per source word (see K_ODO_PRE)
 };
 
+struct TextSet {  // base64 text of each ODO field: t[field][party], 16-byte aligned
+  const char* t[5][kMaxParties];
+};
+
 struct LaunchCfg {
   hipStream_t stream;
   int grid_cap;  // 0 = full grid (one word per thread); > 0 caps it (grid-stride beyond)
@@ -117,6 +121,17 @@ hipError_t launch_synth_odos(const OutSet& out, int n, size_t words, uint64_t se
                              const Fp& f, const LaunchCfg& c);
 hipError_t launch_synth_words(uint4* out, size_t count, uint64_t seed, const Fp& f,
                               const LaunchCfg& c);
+// K_RV / K_MASK straight from the wire: the parties' base64 ODO fields
+// (nchars each = 4 ceil(16 words / 3), `pad` '=' at the end) decoded in the
+// workgroup; bad = min (5 party + field) * nchars + offset of an invalid char.
+hipError_t launch_rv_b64(const TextSet& tx, int n, size_t words, size_t nchars, uint32_t pad,
+                         uint4* out_y, unsigned long long* first_fail, unsigned long long* bad,
+                         const Fp& f, const LaunchCfg& c);
+hipError_t launch_mask_b64(const TextSet& tx, int n, size_t words, size_t nchars, uint32_t pad,
+                           const uint4* secrets, size_t n_secrets, uint4* out16, char* out24,
+                           unsigned long long* first_fail, unsigned long long* bad, const Fp& f,
+                           const LaunchCfg& c);
+
 // Measurement only: K_MASK's memory pattern without the arithmetic.
 hipError_t launch_stream_probe(const OdoSet& odo, int n, size_t words, const uint4* secrets,
                                uint4* out, const LaunchCfg& c);

@@ -278,6 +278,46 @@ int amph_base64_encode_words(amph_ctx* ctx, const uint8_t* words16, size_t words
 int amph_base64_decode_words(amph_ctx* ctx, const char* in24, size_t words, uint8_t* out16,
                              int64_t* bad_index, uint32_t flags, void* stream);
 
+/* ---- K_RV / K_MASK straight from the wire ----------------------------------
+ * The client receives every party's ODO as base64 text -- the secretShares,
+ * rShares, vShares, wShares, uShares strings of the VerifiableSecretShare
+ * (GET /secret-shares/{id}) or OutputDeliveryObject (GET /input-masks) JSON --
+ * and uploads each masked word as a 24-character base64 record
+ * ({"value":"..."} of MaskedInputData).  These calls run the arithmetic of
+ * amph_recombine_verify / amph_mask_input on the text itself: each workgroup
+ * decodes its slice of every field into LDS and consumes it there, so the
+ * decoded words never round-trip through HBM (replaces Jackson's base64
+ * decode of each field + verifyOutputDeliveryObjects, DefaultAmphoraClient.java:
+ * 206-217 / 150-170, MaskedInputData.java:44-52 for the records).
+ *
+ * Every field of every party must be the base64 of exactly 16 * words bytes:
+ * nchars = 4 * ceil(16 * words / 3), '=' padding only in the final group
+ * (else AMPH_E_LEN).  bad_char: the smallest (5 * party + field) * nchars +
+ * offset of a character outside the alphabet (field 0..4 = secretShares,
+ * rShares, vShares, wShares, uShares); -1 / the device sentinel when clean.
+ * Host mode: AMPH_E_PARAM on a bad character (message names party, field
+ * and offset), else AMPH_E_VERIFY as amph_recombine_verify.  Device mode:
+ * text pointers 16-byte aligned, first_fail and bad_char device int64s,
+ * asynchronous on `stream`. */
+typedef struct amph_odo_b64 {
+  const char* secret_shares;
+  const char* r_shares;
+  const char* v_shares;
+  const char* w_shares;
+  const char* u_shares;
+  size_t nchars; /* characters in each of the five strings */
+} amph_odo_b64;
+
+int amph_recombine_verify_b64(amph_ctx* ctx, const amph_odo_b64* odos, int n_parties, size_t words,
+                              uint8_t* out_secrets, int64_t* first_fail, int64_t* bad_char,
+                              uint32_t flags, void* stream);
+/* out_masked16 (16 B per secret) and/or out_records24 (24 base64 characters
+ * per secret, MaskedInputData's value; device: 16-byte aligned) may be NULL. */
+int amph_mask_input_b64(amph_ctx* ctx, const amph_odo_b64* mask_odos, int n_parties, size_t words,
+                        const uint8_t* secrets, size_t n_secrets, uint8_t* out_masked16,
+                        char* out_records24, int64_t* first_fail, int64_t* bad_char, uint32_t flags,
+                        void* stream);
+
 /* ---- Beaver open exchange wire format --------------------------------------
  * MultiplicationExchangeObject.interimValues, the FactorPair list each party
  * sends its partners (amphora-common/.../MultiplicationExchangeObject.java:
