@@ -19,8 +19,8 @@ from typing import List, Sequence
 import numpy as np
 
 from . import _lib
-from .entities import (IntegrityVerificationException, MaskedInput, MaskedInputData,
-                       OutputDeliveryObject, Secret, WORD_WIDTH)
+from .entities import (AmphoraClientException, IntegrityVerificationException, MaskedInput,
+                       MaskedInputData, OutputDeliveryObject, Secret, WORD_WIDTH)
 
 _MASK128 = (1 << 128) - 1
 
@@ -156,6 +156,58 @@ def create_masked_input(util: SecretShareUtil, secret: Secret,
         _raise_for(util, arrays, ff)
     return MaskedInput(secret.secret_id, [MaskedInputData.of(bytes(w)) for w in masked],
                        list(secret.tags))
+
+
+def _texts_and_words(bodies):
+    from . import wire
+    texts = [wire.odo_field_texts(b)[0] for b in bodies]
+    W = wire.words_of_b64(len(texts[0][0]), texts[0][0][-2:])
+    return texts, W
+
+
+def _raise_for_texts(util: SecretShareUtil, texts, i: int):
+    # failure path only: decode the fields and render the reference message
+    arrays = [tuple(_lib.words_view(util.context.base64_decode(t)) for t in ts) for ts in texts]
+    _raise_for(util, arrays, i)
+
+
+def verify_vss_json(util: SecretShareUtil, bodies: Sequence[str]):
+    """getSecret from the parties' VerifiableSecretShare JSON bodies
+    (DefaultAmphoraClient.java:206-217 incl. Jackson's base64 decode of each
+    field): the base64 member strings go to the fused K_RV wire kernel
+    (amph_recombine_verify_b64) as they are.  Returns (secretId, tags,
+    canonical secrets) of the first body."""
+    from . import wire
+    texts, W = _texts_and_words(bodies)
+    try:
+        y, ff, _ = util.context.recombine_verify_b64(texts, W)
+    except ValueError as e:  # an illegal base64 character in some party's body
+        raise AmphoraClientException(str(e)) from e
+    if ff >= 0:
+        _raise_for_texts(util, texts, ff)
+    sid, tags = wire.vss_metadata(bodies[0], wire.odo_field_texts(bodies[0])[1])
+    return sid, tags, unpack(y)
+
+
+def create_masked_input_json(util: SecretShareUtil, secret: Secret, odo_bodies: Sequence[str]) -> str:
+    """createSecret from the parties' OutputDeliveryObject JSON bodies
+    (GET /input-masks) to the MaskedInput JSON body (POST /masked-inputs):
+    verify the masks + maskInput + the per-word base64 records in one fused
+    launch (amph_mask_input_b64)."""
+    from . import wire
+    texts, W = _texts_and_words(odo_bodies)
+    if secret.size() > W:  # verify first, then the index error (as create_masked_input)
+        _, ff, _ = util.context.recombine_verify_b64(texts, W)
+        if ff >= 0:
+            _raise_for_texts(util, texts, ff)
+        raise IndexError("Index %d out of bounds for length %d" % (W, W))
+    try:
+        _, rec, ff, _ = util.context.mask_input_b64(texts, W, pack(secret.data, util.prime), records=True)
+    except ValueError as e:
+        raise AmphoraClientException(str(e)) from e
+    if ff >= 0:
+        _raise_for_texts(util, texts, ff)
+    return wire.records_to_masked_input_json(secret.secret_id, rec, secret.tags)
 
 
 def get_secret_data(util: SecretShareUtil, odos: Sequence[OutputDeliveryObject]) -> List[int]:

@@ -31,7 +31,8 @@ from concurrent.futures import ThreadPoolExecutor
 from typing import Callable, Dict, List, Sequence
 
 from . import _lib
-from .client import SecretShareUtil, create_masked_input, verify_output_delivery_objects
+from .client import (SecretShareUtil, create_masked_input, create_masked_input_json,
+                     verify_output_delivery_objects, verify_vss_json)
 from .entities import (AmphoraClientException, AmphoraServiceException, FactorPair, MaskedInput,
                        MultiplicationExchangeObject, OutputDeliveryObject, Secret, SecretShare)
 from .service import INPUT_MASK_GFP, OutputDeliveryService
@@ -116,9 +117,17 @@ class LoopbackAmphoraClient:
     fanned out concurrently like AmphoraCommunicationClient's parallelStream)."""
 
     def __init__(self, parties: Sequence[AmphoraParty], prime: int, r: int, r_inv: int,
-                 device: int = 0):
+                 device: int = 0, transport: str = "objects"):
+        """transport="json": every hop carries the JSON body the REST API
+        would (OutputDeliveryObject / VerifiableSecretShare / MaskedInput,
+        base64 coded on the parties' GPUs), and the client consumes and
+        produces the text with the fused wire kernels (client.verify_vss_json,
+        client.create_masked_input_json)."""
+        if transport not in ("objects", "json"):
+            raise ValueError("transport must be 'objects' or 'json'")
         self.parties = list(parties)
         self.util = SecretShareUtil.of(prime, r, r_inv, device)
+        self.transport = transport
         self._pool = ThreadPoolExecutor(max_workers=len(self.parties))
 
     @staticmethod
@@ -155,6 +164,14 @@ class LoopbackAmphoraClient:
             raise AmphoraClientException(msg)
 
     def create_secret(self, secret: Secret) -> uuid.UUID:
+        if self.transport == "json":
+            from . import wire
+            bodies = self._unwrap(self._fan_out(lambda p: wire.odo_to_json(
+                p.ctx, p.get_input_masks(secret.secret_id, secret.size()))))
+            text = create_masked_input_json(self.util, secret, bodies)
+            self._check_success(self._fan_out(
+                lambda p: p.upload_masked_input(wire.masked_input_from_json(p.ctx, text))))
+            return secret.secret_id
         odos = self._unwrap(self._fan_out(lambda p: p.get_input_masks(secret.secret_id, secret.size())))
         masked = create_masked_input(self.util, secret, odos)
         self._check_success(self._fan_out(lambda p: p.upload_masked_input(masked)))
@@ -162,6 +179,13 @@ class LoopbackAmphoraClient:
 
     def get_secret(self, secret_id: uuid.UUID) -> Secret:
         request_id = uuid.uuid4()
+        if self.transport == "json":
+            from . import wire
+            bodies = self._unwrap(self._fan_out(lambda p: wire.vss_to_json(
+                p.ctx, secret_id, p.secrets[secret_id].tags, p.get_secret_share(secret_id, request_id),
+                pretty=False)))
+            sid, tags, data = verify_vss_json(self.util, bodies)
+            return Secret(sid, tags, data)
         odos = self._unwrap(self._fan_out(lambda p: p.get_secret_share(secret_id, request_id)))
         data = verify_output_delivery_objects(self.util, odos)
         return Secret(secret_id, list(self.parties[0].secrets[secret_id].tags), data)

@@ -157,6 +157,13 @@ def vss_from_json(ctx: _lib.Context, text: str):
     """JSON -> (secret_id, tags, OutputDeliveryObject); unknown fields ignored
     (VSSDeserializer: FAIL_ON_UNKNOWN_PROPERTIES disabled)."""
     odo, spans = _odo_from_text(ctx, text)
+    sid, tags = vss_metadata(text, spans)
+    return sid, tags, odo
+
+
+def vss_metadata(text: str, spans):
+    """(secretId, tags) of a VerifiableSecretShare body with the ODO member
+    spans cut out (json.loads on the small remainder only)."""
     rest, pos = [], 0
     for s, e in sorted(spans):
         rest.append(text[pos:s])
@@ -171,7 +178,50 @@ def vss_from_json(ctx: _lib.Context, text: str):
     meta = json.loads(small) if small else {}
     if meta.get("secretId") is None:
         raise IllegalArgumentException("secretId is marked non-null but is null")
-    return uuid.UUID(meta["secretId"]), list(meta.get("tags") or []), odo
+    return uuid.UUID(meta["secretId"]), list(meta.get("tags") or [])
+
+
+def odo_field_texts(text: str):
+    """The five base64 member strings of a VerifiableSecretShare /
+    OutputDeliveryObject JSON body, in ODO order, without decoding them (for
+    the fused K_RV / K_MASK wire kernels); also returns the spans removed."""
+    members = _top_level_members(text)
+    vals, spans = [], []
+    for k in ODO_FIELDS:
+        v, s, e = _extract(text, members, k)
+        if v is None:
+            raise IllegalArgumentException("%s is marked non-null but is null" % k)
+        vals.append(v)
+        spans.append((s, e))
+    return vals, spans
+
+
+def words_of_b64(nchars: int, last2: str) -> int:
+    """16-byte words held by a base64 field of nchars characters ending in
+    last2 (its padding); ValueError unless it is a whole number of words."""
+    if nchars % 4:
+        raise ValueError("base64 input length must be a multiple of 4")
+    nbytes = 3 * nchars // 4 - (last2[-2:].count("=") if nchars else 0)
+    if nbytes % 16:
+        raise ValueError("base64 field of %d bytes is not a whole number of 16-byte words" % nbytes)
+    return nbytes // 16
+
+
+def records_to_masked_input_json(secret_id, records, tags) -> str:
+    """MaskedInput JSON from the (W, 24) base64 records of the masked words
+    (what amph_mask_input_b64 writes), framed as masked_input_to_json does."""
+    rec = np.ascontiguousarray(records, np.uint8).reshape(-1, 24)
+    W = rec.shape[0]
+    if W:
+        frame = np.empty((W, 37), np.uint8)
+        frame[:, :10] = np.frombuffer(b'{"value":"', np.uint8)
+        frame[:, 10:34] = rec
+        frame[:, 34:37] = np.frombuffer(b'"},', np.uint8)
+        data = b"[" + frame.tobytes()[:-1] + b"]"
+    else:
+        data = b"[]"
+    tj = json.dumps([_tag_obj(t) for t in tags], separators=(",", ":"))
+    return '{"secretId":"%s","data":%s,"tags":%s}' % (secret_id, data.decode("ascii"), tj)
 
 
 def masked_input_to_json(ctx: _lib.Context, mi: MaskedInput) -> str:

@@ -17,7 +17,7 @@ P, R, RINV = O.TEST_PRIME, O.TEST_R, O.TEST_RINV
 SPDZ = O.MpSpdzIntegrationUtils(P, R, RINV)
 
 
-def _cluster(n, seed, exchange_format="json"):
+def _cluster(n, seed, exchange_format="json", transport="objects"):
     import torch
     assert torch.cuda.is_available()
     from amphora_amd.loopback import AmphoraParty, ExchangeHub, LoopbackAmphoraClient
@@ -27,16 +27,21 @@ def _cluster(n, seed, exchange_format="json"):
     hub = ExchangeHub(n)
     parties = [AmphoraParty(j, P, R, RINV, keys[j], castor, hub, exchange_format=exchange_format)
                for j in range(n)]
-    return LoopbackAmphoraClient(parties, P, R, RINV), parties, keys, castor
+    return LoopbackAmphoraClient(parties, P, R, RINV, transport=transport), parties, keys, castor
 
 
-@pytest.mark.parametrize("n,W,fmt", [(2, 1000, "json"), (3, 257, "json"), (2, 1, "json"),
-                                     (2, 1000, "objects"), (3, 257, "objects")])
-def test_upload_download_roundtrip(n, W, fmt):
+@pytest.mark.parametrize("n,W,fmt,transport", [(2, 1000, "json", "objects"), (3, 257, "json", "objects"),
+                                               (2, 1, "json", "objects"), (2, 1000, "objects", "objects"),
+                                               (3, 257, "objects", "objects"), (2, 1000, "json", "json"),
+                                               (3, 769, "json", "json"), (2, 1, "json", "json"),
+                                               (4, 2, "objects", "json")])
+def test_upload_download_roundtrip(n, W, fmt, transport):
     """fmt: the inter-VCP open carries MultiplicationExchangeObject JSON bodies
-    (GPU-coded) or in-memory FactorPair lists."""
+    (GPU-coded) or in-memory FactorPair lists.  transport="json": the
+    client-party hops carry the REST JSON bodies and the client runs the fused
+    wire kernels (K_RV / K_MASK straight from the base64 text)."""
     import amphora_amd as A
-    client, parties, keys, castor = _cluster(n, seed=W + n, exchange_format=fmt)
+    client, parties, keys, castor = _cluster(n, seed=W + n, exchange_format=fmt, transport=transport)
     rng = random.Random(5)
     data = [rng.randrange(2 ** 63) if i % 2 else rng.randrange(P) for i in range(W)]
     sid = client.create_secret(A.Secret.of([("k", "v")], data))
@@ -61,9 +66,10 @@ def test_upload_download_roundtrip(n, W, fmt):
     client.close()
 
 
-def test_tampered_party_is_detected():
+@pytest.mark.parametrize("transport", ["objects", "json"])
+def test_tampered_party_is_detected(transport):
     import amphora_amd as A
-    client, parties, _, _ = _cluster(2, seed=9)
+    client, parties, _, _ = _cluster(2, seed=9, transport=transport)
     data = list(range(1, 101))
     sid = client.create_secret(A.Secret.of([], data))
     victim = parties[1]
