@@ -128,7 +128,7 @@ __host__ __device__ __forceinline__ uint64_t mad32(uint32_t a, uint32_t b, uint6
 
 // CIOS Montgomery product a * b * 2^-128 mod p.  Requires a < 2^128, b < p
 // (or the symmetric case); returns a canonical value.
-__host__ __device__ __forceinline__ W4 mont_mul(const W4& a, const W4& b, const Fp& f) {
+__host__ __device__ __forceinline__ W4 mont_mul_cios(const W4& a, const W4& b, const Fp& f) {
   uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -148,6 +148,81 @@ __host__ __device__ __forceinline__ W4 mont_mul(const W4& a, const W4& b, const 
     t4 = t5 + (uint32_t)(c >> 32);
   }
   return reduce_once(W4{{t0, t1, t2, t3}}, t4, f);
+}
+
+// acc += a * b on a 96-bit accumulator (lo: 64 bits, hi: 32): one
+// v_mad_u64_u32 whose carry-out (vcc) goes straight into the top word.  The
+// compiler's own lowering of the same sum builds zero-extended 64-bit addends
+// around every mad (v_mov_b32 + 64-bit adds, ~5 instructions per product).
+__host__ __device__ __forceinline__ void macc96(uint64_t& lo, uint32_t& hi, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t out;
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %4\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "=&v"(out), "+v"(hi)
+      : "v"(a), "v"(b), "v"(lo)
+      : "vcc");
+  lo = out;
+#else
+  const uint64_t p = (uint64_t)a * b, s = p + lo;
+  hi += s < p;
+  lo = s;
+#endif
+}
+
+// Product-scanning (FIPS) Montgomery product: column k of a*b and m*p summed
+// in the 96-bit accumulator, m_k chosen as the column's low word comes up,
+// then shifted out.  Same contract as mont_mul_cios (a < 2^128, b < p; the
+// 129-bit result < 2p is reduced once).  ~100 VALU instructions instead of
+// ~165 (tools/ubench/ubench_mm.hip).
+__host__ __device__ __forceinline__ W4 mont_mul_ps(const W4& a, const W4& b, const Fp& f) {
+  uint32_t m[4], r[4];
+  uint64_t lo = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int i = 0; i < k; ++i) {
+      macc96(lo, hi, a.v[i], b.v[k - i]);
+      macc96(lo, hi, m[i], f.p[k - i]);
+    }
+    macc96(lo, hi, a.v[k], b.v[0]);
+    m[k] = (uint32_t)lo * f.n0;
+    macc96(lo, hi, m[k], f.p[0]);  // the low word becomes zero
+    lo = (lo >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+#pragma unroll
+  for (int k = 4; k < 7; ++k) {
+#pragma unroll
+    for (int i = k - 3; i < 4; ++i) {
+      macc96(lo, hi, a.v[i], b.v[k - i]);
+      macc96(lo, hi, m[i], f.p[k - i]);
+    }
+    r[k - 4] = (uint32_t)lo;
+    lo = (lo >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  r[3] = (uint32_t)lo;
+  return reduce_once(W4{{r[0], r[1], r[2], r[3]}}, (uint32_t)(lo >> 32), f);
+}
+
+// The HBM-bound kernels keep the compiler's CIOS lowering: there the VALU
+// work hides under the memory stream anyway, and mont_mul_ps's extra live
+// registers took K_RV at 2 parties from 62 to 66 VGPRs (7 waves per SIMD: one
+// 1024-lane workgroup per CU instead of two, 35.4 vs 33 us at C2).  The
+// VALU-bound wire kernels (k_rv_b64, k_mask_b64) call mont_mul_ps.
+__host__ __device__ __forceinline__ W4 mont_mul(const W4& a, const W4& b, const Fp& f) {
+  return mont_mul_cios(a, b, f);
+}
+
+// Montgomery product for VALU-bound kernels (see above).
+__host__ __device__ __forceinline__ W4 mont_mul_v(const W4& a, const W4& b, const Fp& f) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(AMPH_MONT_CIOS)
+  return mont_mul_ps(a, b, f);
+#else
+  return mont_mul_cios(a, b, f);
+#endif
 }
 
 // Montgomery reduction of a single word: a * 2^-128 mod p (a < 2^128).

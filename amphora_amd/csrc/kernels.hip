@@ -105,6 +105,10 @@ __global__ __launch_bounds__(kMaxBlock) void k_rv(OdoSet odo, int n, size_t word
   }
 }
 
+#ifndef MASK_SECRET_MUL
+#define MASK_SECRET_MUL mont_mul_v
+#endif
+
 // One secret per word (the launcher covers words beyond the secrets with a
 // verify-only k_rv): the secret load is unconditional and issued first, which
 // measured 10 % faster at 3 parties than a per-lane guarded load.
@@ -119,7 +123,9 @@ __global__ __launch_bounds__(kMaxBlock) void k_mask(OdoSet odo, int n, size_t wo
     W4 a[5];
     recombine5<NP, BIG>(odo, n, i, f, a);
     const bool ok = (int)eq(mont_mul(a[0], a[1], f), a[3]) & (int)eq(mont_mul(a[2], a[1], f), a[4]);
-    st(out + i, mod_sub(mont_mul(w4(s), r2, f), a[0], f));
+    // the secret's product in the product-scanning form: 64 instead of 65
+    // VGPRs at 3 parties (8 waves per SIMD: two 1024-lane workgroups per CU)
+    st(out + i, mod_sub(MASK_SECRET_MUL(w4(s), r2, f), a[0], f));
     report_fail(!ok, i, ff);
   }
 }
@@ -583,7 +589,7 @@ __global__ __launch_bounds__(BS) void k_rv_b64(TextSet tx, int n, size_t words, 
     const bool in = word < words;
     bool ok = true;
     if (in) {
-      ok = (int)eq(mont_mul(acc[0], acc[1], f), acc[3]) & (int)eq(mont_mul(acc[2], acc[1], f), acc[4]);
+      ok = (int)eq(mont_mul_v(acc[0], acc[1], f), acc[3]) & (int)eq(mont_mul_v(acc[2], acc[1], f), acc[4]);
       st(out_y + word, redc(acc[0], f));
     }
     report_fail(in && !ok, word, ff);
@@ -619,10 +625,10 @@ __global__ __launch_bounds__(BS) void k_mask_b64(TextSet tx, int n, size_t words
   if (threadIdx.x < WW) {
     const bool in = word < words;
     bool ok = true;
-    if (in) ok = (int)eq(mont_mul(acc[0], acc[1], f), acc[3]) & (int)eq(mont_mul(acc[2], acc[1], f), acc[4]);
+    if (in) ok = (int)eq(mont_mul_v(acc[0], acc[1], f), acc[3]) & (int)eq(mont_mul_v(acc[2], acc[1], f), acc[4]);
     report_fail(in && !ok, word, ff);
     if (has_secret) {
-      const uint4 m = u4(mod_sub(mont_mul(w4(s), r2_word(f), f), acc[0], f));
+      const uint4 m = u4(mod_sub(mont_mul_v(w4(s), r2_word(f), f), acc[0], f));
       if (out16) st(out16 + word, w4(m));
       enc_word24(m, g);
     }
