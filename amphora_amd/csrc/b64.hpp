@@ -57,17 +57,20 @@ __device__ __forceinline__ uint32_t enc_group(uint32_t b0, uint32_t b1, uint32_t
 // 4 base64 chars -> their four 6-bit values (one per byte, same order) and
 // a validity mask (bit 7 of byte j set iff char j is in the alphabet): the
 // table lookups of dec4 without its packing or inverted mask.
+// The '/' class bit of dec4's tables is widened to two bits (HI[2] = 0x31,
+// LO[15] = 0x35), so '/' reads 3 in bits 4-5 of its class and the -3 it
+// needs after the ROLL add is (cls >> 4) & 3 -- no multiply by 3 (which the
+// compiler emitted as a quarter-rate v_mul_lo_u32 per group).
 __device__ __forceinline__ uint32_t dec4_values(uint32_t w, uint32_t& valid) {
   const uint32_t lo = w & 0x0F0F0F0Fu, l7 = lo & 0x07070707u, h7 = (w >> 4) & 0x07070707u;
   const uint32_t la = __builtin_amdgcn_perm(0x0E0E0E0Eu, 0x0E0E0E0Au, l7);
-  const uint32_t lb = __builtin_amdgcn_perm(0x15040404u, 0x050C0E0Eu, l7);
+  const uint32_t lb = __builtin_amdgcn_perm(0x35040404u, 0x050C0E0Eu, l7);
   const uint32_t cl = __builtin_amdgcn_perm(lb, la, 0x03020100u | ((lo & 0x08080808u) >> 1));
-  const uint32_t cls = __builtin_amdgcn_perm(0x08040804u, 0x02110000u, h7) & cl;
+  const uint32_t cls = __builtin_amdgcn_perm(0x08040804u, 0x02310000u, h7) & cl;
   valid = ((cls & 0x0F0F0F0Fu) + 0x7F7F7F7Fu) & ~w;  // bit 7: in the alphabet (and ASCII)
   const uint32_t roll = __builtin_amdgcn_perm(0xB9B9BFBFu, 0x04130000u, h7);
-  uint32_t v = ((w & 0x7F7F7F7Fu) + (roll & 0x7F7F7F7Fu)) ^ ((w ^ roll) & 0x80808080u);
-  const uint32_t fix = (cls >> 4) & 0x01010101u;
-  return v - (fix + (fix << 1));
+  const uint32_t v = ((w & 0x7F7F7F7Fu) + (roll & 0x7F7F7F7Fu)) ^ ((w ^ roll) & 0x80808080u);
+  return v - ((cls >> 4) & 0x03030303u);  // no borrow: '/' + ROLL = 66 per byte
 }
 
 // One full 16-character unit (4 groups, no padding) -> its 12 bytes as 3

@@ -514,9 +514,16 @@ __device__ __forceinline__ uint32_t dec_unit_slow(const char* t, size_t unit, si
 
 // Sum field k over the parties from the text, consuming it through LDS.  raw:
 // this lane's units, loaded up front on the fast path (FAST).
+// Fast-path loads: kWirePrefetch > 0 issues field f + kWirePrefetch's load
+// while field f is decoded (fewer live VGPRs); 0 issues all 5N up front.
+#ifndef AMPH_WIRE_PD
+#define AMPH_WIRE_PD 0
+#endif
+constexpr int kWirePrefetch = AMPH_WIRE_PD;
+
 template <int NP, bool BIG, bool FAST, int BS>
 __device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nchars, uint32_t pad,
-                                            size_t words, const uint4 (&raw)[5][NP > 0 ? NP : 1],
+                                            size_t words, uint4 (&raw)[5][NP > 0 ? NP : 1],
                                             uint32_t (*lds)[3 * BS], W4 (&acc)[5],
                                             unsigned long long* bad, const Fp& f) {
   const size_t unit = (size_t)blockIdx.x * BS + threadIdx.x;
@@ -532,6 +539,11 @@ __device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nch
       uint32_t o[3];
       uint32_t fb;
       if constexpr (FAST && NP > 0) {
+        if constexpr (kWirePrefetch > 0) {
+          const int ahead = k * NP + j + kWirePrefetch;
+          if (ahead < 5 * NP)
+            raw[ahead / NP][ahead % NP] = ld(reinterpret_cast<const uint4*>(tx.t[ahead / NP][ahead % NP]) + unit);
+        }
         fb = dec_unit16(raw[k][j], o);
       } else if constexpr (FAST) {
         fb = dec_unit16(ld(reinterpret_cast<const uint4*>(tx.t[k][j]) + unit), o);
@@ -562,7 +574,9 @@ __device__ __forceinline__ void wire_load(const TextSet& tx, uint4 (&raw)[5][NP 
 #pragma unroll
     for (int k = 0; k < 5; ++k)
 #pragma unroll
-      for (int j = 0; j < NP; ++j) raw[k][j] = ld(reinterpret_cast<const uint4*>(tx.t[k][j]) + unit);
+      for (int j = 0; j < NP; ++j)
+        if (kWirePrefetch == 0 || k * NP + j < kWirePrefetch)
+          raw[k][j] = ld(reinterpret_cast<const uint4*>(tx.t[k][j]) + unit);
   }
 }
 
