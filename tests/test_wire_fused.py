@@ -154,3 +154,37 @@ def test_mask_b64_matches_oracle(ctx, F, mode, n, W, S):
     if mode == "host":
         _, _, ff, _ = ctx.mask_input_b64(texts_of(odos), W, secrets)
         assert ff == fault
+
+
+@pytest.mark.parametrize("n,W", [(2, 1 << 20), (3, 1 << 24), (2, 1 << 26)])
+def test_wire_kernels_at_baseline_sizes(ctx, n, W):
+    """C2, C3 and the whole of C4 on one GPU: the parties' fields base64-coded
+    on the GPU, then K_RV / K_MASK from the text must equal K_RV / K_MASK on
+    the words (every output word), and an injected MAC fault is found at its
+    index -- size-independent properties at the sizes BASELINE names."""
+    import torch
+    nf = 0x7F7F7F7F7F7F7F7F
+    odos, buf, _ = ctx.synth_odos(seed=77, n=n, words=W, noncanon_permille=5)
+    texts = [[ctx.base64_encode(f.reshape(-1)) for f in o] for o in odos]
+    y_ref, ff_ref = ctx.recombine_verify(odos)
+    y, ff, bad = ctx.recombine_verify_b64(texts, W)
+    torch.cuda.synchronize()
+    assert int(ff.item()) == int(ff_ref.item()) == nf and int(bad.item()) == nf
+    assert torch.equal(y, y_ref)
+    del y, y_ref
+    secrets = ctx.synth_words(seed=78, count=W)
+    m_ref, _ = ctx.mask_input(odos, secrets)
+    m16, rec, ff, bad = ctx.mask_input_b64(texts, W, secrets, records=True, raw=True)
+    torch.cuda.synchronize()
+    assert int(ff.item()) == nf and int(bad.item()) == nf and torch.equal(m16, m_ref)
+    assert torch.equal(rec, ctx.base64_encode_words(m_ref))
+    del m16, rec, m_ref, secrets, texts
+    # a MAC fault in party 1's w field, re-encoded
+    fault = (2 * W) // 3
+    odos[1][3][fault, 0] ^= 1
+    texts = [[ctx.base64_encode(f.reshape(-1)) for f in o] for o in odos]
+    _, ff, bad = ctx.recombine_verify_b64(texts, W)
+    torch.cuda.synchronize()
+    assert int(ff.item()) == fault and int(bad.item()) == nf
+    del buf, odos, texts
+    torch.cuda.empty_cache()
