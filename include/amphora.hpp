@@ -44,6 +44,9 @@ struct IllegalArgumentException : std::invalid_argument {
 struct AmphoraServiceException : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
+struct AmphoraClientException : std::runtime_error {  // amphora-common AmphoraClientException
+  using std::runtime_error::runtime_error;
+};
 struct NativeError : std::runtime_error {
   int status;
   NativeError(int st, const std::string& m) : std::runtime_error(m), status(st) {}
@@ -285,6 +288,79 @@ inline std::vector<Bytes> maskSecret(const SecretShareUtil& util, const std::vec
   std::vector<Bytes> words;
   for (size_t i = 0; i < s.size(); ++i) words.emplace_back(out.begin() + 16 * i, out.begin() + 16 * i + 16);
   return words;
+}
+
+// The five base64 field strings of one party's VerifiableSecretShare /
+// OutputDeliveryObject JSON body (secretShares, rShares, vShares, wShares,
+// uShares), kept as text: the client hands them to the fused wire kernels.
+struct OdoText {
+  std::string f[5];
+  amph_odo_b64 view() const {
+    return amph_odo_b64{f[0].data(), f[1].data(), f[2].data(), f[3].data(), f[4].data(), f[0].size()};
+  }
+};
+
+inline size_t wordsOfBase64(const std::string& t) {
+  const size_t pad = t.size() >= 2 ? (t[t.size() - 1] == '=') + (t[t.size() - 2] == '=') : 0;
+  const size_t nb = t.size() / 4 * 3 - pad;
+  if (t.size() % 4 || nb % 16) throw IllegalArgumentException("base64 field is not a whole number of words");
+  return nb / 16;
+}
+
+// getSecret from the parties' response text (DefaultAmphoraClient.java:206-217
+// incl. the base64 decode Jackson does per field): one launch of
+// amph_recombine_verify_b64; a bad character -> AmphoraClientException.
+inline std::vector<u128> verifyOutputDeliveryText(const SecretShareUtil& util,
+                                                  const std::vector<OdoText>& odos) {
+  std::vector<amph_odo_b64> v;
+  for (auto& o : odos) v.push_back(o.view());
+  const size_t W = odos.empty() ? 0 : wordsOfBase64(odos[0].f[0]);
+  Bytes out(W * 16);
+  int64_t ff = -1, bad = -1;
+  const int st = amph_recombine_verify_b64(util.context().get(), v.data(), (int)v.size(), W, out.data(),
+                                           &ff, &bad, 0, nullptr);
+  if (st == AMPH_E_PARAM && bad >= 0) throw AmphoraClientException(amph_last_error());
+  if (st == AMPH_E_VERIFY) {  // the reference message, from the decoded fields
+    std::vector<OutputDeliveryObject> dec;
+    for (auto& o : odos) {
+      Bytes f[5];
+      for (int k = 0; k < 5; ++k) {
+        f[k].resize(3 * o.f[k].size() / 4);
+        size_t nb = 0;
+        int64_t b2 = -1;
+        check(amph_base64_decode(util.context().get(), o.f[k].data(), o.f[k].size(), f[k].data(), &nb, &b2, 0,
+                                 nullptr));
+        f[k].resize(nb);
+      }
+      dec.emplace_back(f[0], f[1], f[2], f[3], f[4]);
+    }
+    verifyOutputDeliveryObjects(util, dec);  // throws IntegrityVerificationException
+  }
+  check(st);
+  return unpackWords(out);
+}
+
+// createSecret from the parties' /input-masks response text: verify + mask +
+// the MaskedInputData base64 records (24 characters per word), one launch of
+// amph_mask_input_b64.
+inline std::vector<std::string> maskSecretText(const SecretShareUtil& util, const std::vector<u128>& secret,
+                                               const std::vector<OdoText>& maskOdos) {
+  std::vector<amph_odo_b64> v;
+  for (auto& o : maskOdos) v.push_back(o.view());
+  const size_t W = maskOdos.empty() ? 0 : wordsOfBase64(maskOdos[0].f[0]);
+  std::vector<u128> s(secret);
+  for (auto& x : s) x %= util.getPrime();
+  Bytes in = packWords(s);
+  std::string rec(24 * s.size(), '\0');
+  int64_t ff = -1, bad = -1;
+  const int st = amph_mask_input_b64(util.context().get(), v.data(), (int)v.size(), W, in.data(), s.size(),
+                                     nullptr, &rec[0], &ff, &bad, 0, nullptr);
+  if (st == AMPH_E_PARAM && bad >= 0) throw AmphoraClientException(amph_last_error());
+  if (st == AMPH_E_VERIFY) verifyOutputDeliveryText(util, maskOdos);  // throws with the message
+  check(st);
+  std::vector<std::string> out;
+  for (size_t i = 0; i < s.size(); ++i) out.push_back(rec.substr(24 * i, 24));
+  return out;
 }
 
 }  // namespace client

@@ -196,6 +196,32 @@ static void gpu_tests() {
     threw = true;
   }
   EXPECT(threw);
+  // the same round trip from the response text (fused wire kernels)
+  std::vector<client::OdoText> texts(2);
+  for (int j = 0; j < 2; ++j)
+    for (int k = 0; k < 5; ++k) texts[j].f[k] = wire::base64Encode(c, parts[j][k]);
+  EXPECT(client::verifyOutputDeliveryText(util, texts) == sec);
+  auto records = client::maskSecretText(util, secrets, texts);
+  EXPECT(records.size() == W);
+  for (size_t i = 0; i < W; i += 97) EXPECT(records[i] == wire::base64Encode(c, maskedWords[i]));
+  auto tamperedText = texts;
+  tamperedText[1].f[3] = wire::base64Encode(c, wt);
+  threw = false;
+  try {
+    client::verifyOutputDeliveryText(util, tamperedText);
+  } catch (const IntegrityVerificationException& e) {
+    threw = std::string(e.what()).rfind("Verification of secret has failed", 0) == 0;
+  }
+  EXPECT(threw);
+  auto badChar = texts;
+  badChar[0].f[2][100] = '*';
+  threw = false;
+  try {
+    client::verifyOutputDeliveryText(util, badChar);
+  } catch (const AmphoraClientException& e) {
+    threw = std::string(e.what()).find("index 100 of party 0's vShares") != std::string::npos;
+  }
+  EXPECT(threw);
 }
 
 int main(int argc, char** argv) {
