@@ -196,6 +196,22 @@ struct HostOut {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Results of a one-shot host call: wait for the stream, then copy with
+// blocking hipMemcpy.  (A small hipMemcpyAsync into pageable host memory --
+// a verdict word on the stack -- was once seen to hold a value from before
+// the kernel on the same stream; the copies below cannot.)
+struct ReadBack {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+hipError_t read_back(hipStream_t s, std::initializer_list<ReadBack> copies) {
+  hipError_t e = hipStreamSynchronize(s);
+  for (const ReadBack& r : copies)
+    if (e == hipSuccess && r.bytes) e = hipMemcpy(r.dst, r.src, r.bytes, hipMemcpyDeviceToHost);
+  return e;
+}
+
 int host_threads() {
   if (const char* t = std::getenv("AMPH_HOST_THREADS")) return std::max(1, std::atoi(t));
   const unsigned hw = std::thread::hardware_concurrency();
@@ -1007,9 +1023,7 @@ int run_tail(amph_ctx* c, const void* in, size_t in_bytes, void* out, size_t out
   if (with_bad) HIP_TRY(hipMemsetAsync(d + 448, 0x7F, 8, s));
   e = launch(d, d + 256, (unsigned long long*)(d + 448), cfg(c, s, 1));
   if (e != hipSuccess) return hip_fail(e, "codec tail");
-  HIP_TRY(hipMemcpyAsync(out, d + 256, out_bytes, hipMemcpyDeviceToHost, s));
-  if (with_bad) HIP_TRY(hipMemcpyAsync(bad_host, d + 448, 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(read_back(s, {{out, d + 256, out_bytes}, {bad_host, d + 448, with_bad ? (size_t)8 : 0}}));
   return AMPH_OK;
 }
 }  // namespace
@@ -1054,8 +1068,7 @@ int amph_base64_decode(amph_ctx* c, const char* in, size_t nchars, uint8_t* out,
     HIP_TRY(hipSetDevice(c->device));
     if (!bad_index) return fail(AMPH_E_PARAM, "bad_index is required");
     // one 2-byte read-back decides the padding (the only synchronous step)
-    HIP_TRY(hipMemcpyAsync(last2, in + nchars - 2, 2, hipMemcpyDeviceToHost, (hipStream_t)stream));
-    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(read_back((hipStream_t)stream, {{last2, in + nchars - 2, 2}}));
     const size_t ob = 3 * nchars / 4 - b64_padding(last2);
     if (out_bytes) *out_bytes = ob;
     if (int st = reset_ff_dev(bad_index, flags, (hipStream_t)stream)) return st;
@@ -1202,13 +1215,11 @@ int amph_exchange_encode(amph_ctx* c, const uint8_t* mag16, const uint8_t* neg, 
                                               cfg(c, s, npairs));
   if (e != hipSuccess) return hip_fail(e, "k_xenc");
   uint64_t len = 0;
-  HIP_TRY(hipMemcpyAsync(&len, dlen.p, 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(read_back(s, {{&len, dlen.p, 8}}));
   *out_len = len;
   if (len > out_cap) return fail(AMPH_E_LEN, "output capacity " + std::to_string(out_cap) +
                                                  " below the encoded length " + std::to_string(len));
-  HIP_TRY(hipMemcpyAsync(out, dout.p, len, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(read_back(s, {{out, dout.p, len}}));
   return AMPH_OK;
 }
 
@@ -1243,8 +1254,7 @@ int amph_exchange_decode(amph_ctx* c, const char* text, size_t len, size_t npair
                                               cfg(c, s, len));
   if (e != hipSuccess) return hip_fail(e, "k_xdec");
   int64_t bad = 0;
-  HIP_TRY(hipMemcpyAsync(&bad, dbad.p, 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(read_back(s, {{&bad, dbad.p, 8}}));
   const bool ok = bad == (int64_t)AMPH_NO_FAILURE;
   if (bad_index) *bad_index = ok ? -1 : bad;
   if (!ok) {
@@ -1252,11 +1262,7 @@ int amph_exchange_decode(amph_ctx* c, const char* text, size_t len, size_t npair
       return fail(AMPH_E_LEN, "interimValues must hold exactly " + std::to_string(npairs) + " FactorPairs");
     return fail(AMPH_E_PARAM, "Malformed FactorPair JSON at offset " + std::to_string(bad));
   }
-  if (npairs) {
-    HIP_TRY(hipMemcpyAsync(mag16, dmag.p, 32 * npairs, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(neg, dneg.p, 2 * npairs, hipMemcpyDeviceToHost, s));
-  }
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(read_back(s, {{mag16, dmag.p, 32 * npairs}, {neg, dneg.p, 2 * npairs}}));
   return AMPH_OK;
 }
 
@@ -1358,9 +1364,7 @@ int amph_recombine_verify_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size
                                      cfg(c, s, words));
   if (e != hipSuccess) return hip_fail(e, "k_rv_b64");
   int64_t v[2];
-  HIP_TRY(hipMemcpyAsync(v, fl, 16, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(out_secrets, h.out.p, 16 * words, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(read_back(s, {{v, fl, 16}, {out_secrets, h.out.p, 16 * words}}));
   if (v[1] != (int64_t)AMPH_NO_FAILURE) {
     if (bad_char) *bad_char = v[1];
     return wire_bad_message(v[1], nchars);
@@ -1416,10 +1420,8 @@ int amph_mask_input_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size_t wor
                                        fl, fl + 1, c->f, cfg(c, s, words));
   if (e != hipSuccess) return hip_fail(e, "k_mask_b64");
   int64_t v[2];
-  HIP_TRY(hipMemcpyAsync(v, fl, 16, hipMemcpyDeviceToHost, s));
-  if (out16 && n_secrets) HIP_TRY(hipMemcpyAsync(out16, h.out.p, 16 * n_secrets, hipMemcpyDeviceToHost, s));
-  if (out24 && n_secrets) HIP_TRY(hipMemcpyAsync(out24, h.out2.p, 24 * n_secrets, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(read_back(s, {{v, fl, 16}, {out16, h.out.p, out16 ? 16 * n_secrets : 0},
+                        {out24, h.out2.p, out24 ? 24 * n_secrets : 0}}));
   if (v[1] != (int64_t)AMPH_NO_FAILURE) {
     if (bad_char) *bad_char = v[1];
     return wire_bad_message(v[1], nchars);

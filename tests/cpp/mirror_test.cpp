@@ -200,7 +200,10 @@ static void gpu_tests() {
   std::vector<client::OdoText> texts(2);
   for (int j = 0; j < 2; ++j)
     for (int k = 0; k < 5; ++k) texts[j].f[k] = wire::base64Encode(c, parts[j][k]);
-  EXPECT(client::verifyOutputDeliveryText(util, texts) == sec);
+  for (int rep = 0; rep < 16; ++rep) {  // repeated one-shot host calls (fresh staging each time)
+    EXPECT(client::verifyOutputDeliveryText(util, texts) == sec);
+    EXPECT(client::maskSecretText(util, secrets, texts).size() == W);
+  }
   auto records = client::maskSecretText(util, secrets, texts);
   EXPECT(records.size() == W);
   for (size_t i = 0; i < W; i += 97) EXPECT(records[i] == wire::base64Encode(c, maskedWords[i]));
