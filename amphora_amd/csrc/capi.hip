@@ -365,6 +365,11 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
   for (size_t b = nb > (size_t)S ? nb - S : 0; b < nb; ++b)
     if (int rc = drain_out(c->slots[b % S])) return rc;
   HIP_TRY(hipStreamSynchronize(s_out));  // page-locked outputs (no staging slot) landed too
+  // a call with no outputs (amph_verify, the verify-only tail of
+  // amph_mask_input) has nothing on s_out that waits for its kernels: wait
+  // for them before the verdicts are read (the blocking copy below runs on
+  // the null stream, which does not order with non-blocking streams)
+  HIP_TRY(hipStreamSynchronize(s_k));
   if (with_ff) {
     std::vector<unsigned long long> h(nb);
     HIP_TRY(hipMemcpy(h.data(), c->ff.p, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost));
