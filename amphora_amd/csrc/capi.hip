@@ -122,6 +122,7 @@ struct amph_ctx {
   std::vector<amph_ctx*> sub;  // amph_ctx_create_multi: one context per device
   DevBuf ff;  // per-batch first-fail words (host path)
   DevBuf tail;  // small scratch for the partial last unit of codec calls
+  DevBuf wire;  // host-mode staging of the wire-text calls (texts, secrets, outputs, verdicts)
   std::unique_ptr<amph::CopyPool> pool;
 };
 
@@ -621,6 +622,7 @@ void amph_ctx_destroy(amph_ctx* c) {
     }
     c->ff.release();
     c->tail.release();
+    c->wire.release();
   }
   delete c;
 }
@@ -1211,9 +1213,10 @@ int amph_exchange_encode(amph_ctx* c, const uint8_t* mag16, const uint8_t* neg, 
   HIP_TRY(dout.alloc(maxb, s));
   HIP_TRY(dlen.alloc(8, s));
   HIP_TRY(scratch.alloc(amph::xenc_scratch_bytes(npairs), s));
+  HIP_TRY(hipStreamSynchronize(s));  // the stream-ordered allocations exist; blocking copies in
   if (npairs) {
-    HIP_TRY(hipMemcpyAsync(dmag.p, mag16, 32 * npairs, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(dneg.p, neg, 2 * npairs, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpy(dmag.p, mag16, 32 * npairs, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dneg.p, neg, 2 * npairs, hipMemcpyHostToDevice));
   }
   hipError_t e = amph::launch_exchange_encode((const uint4*)dmag.p, (const uint8_t*)dneg.p, npairs,
                                               (char*)dout.p, (unsigned long long*)dlen.p, scratch.p,
@@ -1252,7 +1255,8 @@ int amph_exchange_decode(amph_ctx* c, const char* text, size_t len, size_t npair
   HIP_TRY(dneg.alloc(2 * npairs, s));
   HIP_TRY(dbad.alloc(8, s));
   HIP_TRY(scratch.alloc(amph::xdec_scratch_bytes(len), s));
-  if (len) HIP_TRY(hipMemcpyAsync(dtext.p, text, len, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));  // the stream-ordered allocations exist; blocking copy in
+  if (len) HIP_TRY(hipMemcpy(dtext.p, text, len, hipMemcpyHostToDevice));
   HIP_TRY(hipMemsetAsync(dbad.p, 0x7F, 8, s));
   hipError_t e = amph::launch_exchange_decode((const char*)dtext.p, len, npairs, (uint4*)dmag.p,
                                               (uint8_t*)dneg.p, (unsigned long long*)dbad.p, scratch.p,
@@ -1309,22 +1313,34 @@ int wire_bad_message(int64_t bad, size_t nchars) {
                                 std::to_string(o / 5) + "'s " + kOdoFieldNames[o % 5]);
 }
 
-// Host mode: the texts go to the device in one copy each (no batching: the
-// whole call is one launch), outputs come back, verdicts are read.
+// Host mode: the texts go to the device in one blocking copy each into the
+// context's staging buffer (no batching: the whole call is one launch), the
+// kernel runs on the context's stream, and the results come back after it.
+// (A first version staged through stream-ordered hipMallocAsync memory with
+// pageable hipMemcpyAsync; in a fresh process its first call intermittently
+// saw the first text unit unwritten.)
 struct WireHost {
-  AsyncBuf text, out, out2, words16, flags;
   amph::TextSet tx{};
-  int stage(const amph_odo_b64* odos, int n, size_t nchars, hipStream_t s) {
-    const size_t stride = (nchars + 15) & ~(size_t)15;
-    HIP_TRY(text.alloc(5 * n * stride, s));
+  uint8_t* base = nullptr;
+  size_t off = 0;
+  uint8_t* take(size_t bytes) {
+    uint8_t* p = base + off;
+    off += align256(bytes ? bytes : 16);
+    return p;
+  }
+  static size_t bytes_for(int n, size_t nchars, size_t extra) {
+    return 5 * n * align256(nchars ? nchars : 16) + extra + 256;
+  }
+  int stage(amph_ctx* c, const amph_odo_b64* odos, int n, size_t nchars, size_t extra) {
+    hipError_t e = c->wire.ensure(bytes_for(n, nchars, extra));
+    if (e != hipSuccess) return fail(AMPH_E_NOMEM, "wire staging");
+    base = (uint8_t*)c->wire.p;
     for (int j = 0; j < n; ++j)
       for (int k = 0; k < 5; ++k) {
-        char* d = (char*)text.p + (5 * j + k) * stride;
-        if (nchars) HIP_TRY(hipMemcpyAsync(d, b64_field(odos[j], k), nchars, hipMemcpyHostToDevice, s));
-        tx.t[k][j] = d;
+        uint8_t* d = take(nchars);
+        if (nchars) HIP_TRY(hipMemcpy(d, b64_field(odos[j], k), nchars, hipMemcpyHostToDevice));
+        tx.t[k][j] = (const char*)d;
       }
-    HIP_TRY(flags.alloc(16, s));
-    HIP_TRY(hipMemsetAsync(flags.p, 0x7F, 16, s));
     return AMPH_OK;
   }
 };
@@ -1362,14 +1378,15 @@ int amph_recombine_verify_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size
   hipStream_t s;
   if (int st = host_stream0(c, &s)) return st;
   WireHost h;
-  if (int st = h.stage(odos, n, nchars, s)) return st;
-  HIP_TRY(h.out.alloc(16 * words, s));
-  unsigned long long* fl = (unsigned long long*)h.flags.p;
-  hipError_t e = amph::launch_rv_b64(h.tx, n, words, nchars, pad, (uint4*)h.out.p, fl, fl + 1, c->f,
+  if (int st = h.stage(c, odos, n, nchars, align256(16 * words) + 256)) return st;
+  uint8_t* dout = h.take(16 * words);
+  unsigned long long* fl = (unsigned long long*)h.take(16);
+  HIP_TRY(hipMemsetAsync(fl, 0x7F, 16, s));
+  hipError_t e = amph::launch_rv_b64(h.tx, n, words, nchars, pad, (uint4*)dout, fl, fl + 1, c->f,
                                      cfg(c, s, words));
   if (e != hipSuccess) return hip_fail(e, "k_rv_b64");
   int64_t v[2];
-  HIP_TRY(read_back(s, {{v, fl, 16}, {out_secrets, h.out.p, 16 * words}}));
+  HIP_TRY(read_back(s, {{v, fl, 16}, {out_secrets, dout, 16 * words}}));
   if (v[1] != (int64_t)AMPH_NO_FAILURE) {
     if (bad_char) *bad_char = v[1];
     return wire_bad_message(v[1], nchars);
@@ -1414,19 +1431,21 @@ int amph_mask_input_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size_t wor
   hipStream_t s;
   if (int st = host_stream0(c, &s)) return st;
   WireHost h;
-  if (int st = h.stage(odos, n, nchars, s)) return st;
-  HIP_TRY(h.words16.alloc(16 * n_secrets, s));
-  if (n_secrets) HIP_TRY(hipMemcpyAsync(h.words16.p, secrets, 16 * n_secrets, hipMemcpyHostToDevice, s));
-  if (out16) HIP_TRY(h.out.alloc(16 * n_secrets, s));
-  if (out24) HIP_TRY(h.out2.alloc(24 * n_secrets, s));
-  unsigned long long* fl = (unsigned long long*)h.flags.p;
-  hipError_t e = amph::launch_mask_b64(h.tx, n, words, nchars, pad, (const uint4*)h.words16.p, n_secrets,
-                                       out16 ? (uint4*)h.out.p : nullptr, out24 ? (char*)h.out2.p : nullptr,
+  const size_t extra = 3 * align256(16 * n_secrets) + align256(24 * n_secrets) + 1024;
+  if (int st = h.stage(c, odos, n, nchars, extra)) return st;
+  uint8_t* dsec = h.take(16 * n_secrets);
+  uint8_t* d16 = h.take(16 * n_secrets);
+  uint8_t* d24 = h.take(24 * n_secrets);
+  unsigned long long* fl = (unsigned long long*)h.take(16);
+  if (n_secrets) HIP_TRY(hipMemcpy(dsec, secrets, 16 * n_secrets, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemsetAsync(fl, 0x7F, 16, s));
+  hipError_t e = amph::launch_mask_b64(h.tx, n, words, nchars, pad, (const uint4*)dsec, n_secrets,
+                                       out16 ? (uint4*)d16 : nullptr, out24 ? (char*)d24 : nullptr,
                                        fl, fl + 1, c->f, cfg(c, s, words));
   if (e != hipSuccess) return hip_fail(e, "k_mask_b64");
   int64_t v[2];
-  HIP_TRY(read_back(s, {{v, fl, 16}, {out16, h.out.p, out16 ? 16 * n_secrets : 0},
-                        {out24, h.out2.p, out24 ? 24 * n_secrets : 0}}));
+  HIP_TRY(read_back(s, {{v, fl, 16}, {out16, d16, out16 ? 16 * n_secrets : 0},
+                        {out24, d24, out24 ? 24 * n_secrets : 0}}));
   if (v[1] != (int64_t)AMPH_NO_FAILURE) {
     if (bad_char) *bad_char = v[1];
     return wire_bad_message(v[1], nchars);

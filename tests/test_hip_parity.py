@@ -525,3 +525,20 @@ def test_stream_probe_pattern(ctx, F):
                 exp ^= f
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy(), exp), n
+
+
+def test_host_verdicts_follow_the_kernels(ctx, F):
+    """Host-pointer calls whose only result is the verdict (amph_verify; the
+    verify-only tail of amph_mask_input) report a fault in the LAST words of
+    the last batch every time: the verdict is read only after the kernels."""
+    W = 200_003
+    odos, _ = F.synth_odos(seed=1300, n=2, W=W, fault_index=W - 1)
+    secrets = F.synth_words(seed=1301, count=1000, mont=False)
+    y, r, v, w, u = (np.ascontiguousarray(F.recombine([o[k] for o in odos])) for k in range(5))
+    ctx.set_batch_words(65_536)
+    try:
+        for _ in range(12):
+            assert ctx.verify(y, r, u, v, w) == W - 1
+            assert ctx.mask_input(odos, secrets)[1] == W - 1
+    finally:
+        ctx.set_batch_words(4 << 20)
