@@ -535,6 +535,9 @@ def main():
                                  "recorded right before and after the call (hipEventRecord)",
                                  ns, a.steps)),
             "kernels_gbs": {k: round(kbytes(k, n) * W / (v * 1e-3) / 1e9, 1) for k, v in kern.items()},
+            # share-encode and recombine+verify rates separately
+            # (per GPU, from the kernel timings); `value` is the round trip
+            "kernels_words_per_s": {k: round(W / (v * 1e-3)) for k, v in kern.items()},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "bytes_per_word": bpw, "traffic": traffic},
