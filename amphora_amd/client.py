@@ -20,7 +20,7 @@ import numpy as np
 
 from . import _lib
 from .entities import (AmphoraClientException, IntegrityVerificationException, MaskedInput,
-                       MaskedInputData, OutputDeliveryObject, Secret, WORD_WIDTH)
+                       MaskedInputData, MaskedInputWords, OutputDeliveryObject, Secret, WORD_WIDTH)
 
 _MASK128 = (1 << 128) - 1
 
@@ -154,8 +154,7 @@ def create_masked_input(util: SecretShareUtil, secret: Secret,
     masked, ff = util.context.mask_input(arrays, pack(secret.data, util.prime))
     if ff >= 0:
         _raise_for(util, arrays, ff)
-    return MaskedInput(secret.secret_id, [MaskedInputData.of(bytes(w)) for w in masked],
-                       list(secret.tags))
+    return MaskedInput(secret.secret_id, MaskedInputWords(masked), list(secret.tags))
 
 
 def _texts_and_words(bodies):

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import uuid
 from dataclasses import dataclass, field
+from collections.abc import Sequence
 from typing import List, Optional
 
 WORD_WIDTH = 16
@@ -82,6 +83,32 @@ class MaskedInputData:
             raise IllegalArgumentException(
                 "Length of a Masked Input value has to be %d bytes." % WORD_WIDTH)
         return MaskedInputData(bytes(value))
+
+
+class MaskedInputWords(Sequence):
+    """List<MaskedInputData> backed by one (W, 16) uint8 array: the masked
+    words as the kernels write them, materialised as MaskedInputData only
+    when an element is read (the host mirror hands the array itself to the
+    next kernel or codec instead of W Python objects)."""
+
+    def __init__(self, words):
+        import numpy as np
+        w = np.ascontiguousarray(words, np.uint8)
+        if w.ndim != 2 or w.shape[1] != WORD_WIDTH:
+            raise IllegalArgumentException(
+                "Length of a Masked Input value has to be %d bytes." % WORD_WIDTH)
+        self.words = w
+
+    def __len__(self):
+        return self.words.shape[0]
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return MaskedInputWords(self.words[i])
+        return MaskedInputData(self.words[i].tobytes())
+
+    def __eq__(self, other):
+        return list(self) == list(other)
 
 
 @dataclass

@@ -55,8 +55,12 @@ class SecretShareUtil:
         masks = _tuples(input_masks, 32)
         if len(masked_input.data) != masks.shape[0]:
             raise IllegalArgumentException("Received more input data than available inputMasks.")
-        masked = np.frombuffer(b"".join(d.value for d in masked_input.data), np.uint8).reshape(-1, 16) \
-            if masked_input.data else np.zeros((0, 16), np.uint8)
+        data = masked_input.data
+        if hasattr(data, "words"):  # MaskedInputWords: the array itself
+            masked = data.words
+        else:
+            masked = np.frombuffer(b"".join(d.value for d in data), np.uint8).reshape(-1, 16) \
+                if data else np.zeros((0, 16), np.uint8)
         key = int(mac_key) % self._ctx.prime  # new BigInteger(mac) :86 (used mod p)
         out = self._ctx.convert_share(masked, masks, key, use_zero_input_as_data)
         return SecretShare(masked_input.secret_id, out.tobytes(), list(masked_input.tags))

@@ -25,7 +25,7 @@ from typing import List, Tuple
 import numpy as np
 
 from . import _lib
-from .entities import (IllegalArgumentException, MaskedInput, MaskedInputData,
+from .entities import (IllegalArgumentException, MaskedInput, MaskedInputData, MaskedInputWords,
                        OutputDeliveryObject)
 
 ODO_FIELDS = ("secretShares", "rShares", "vShares", "wShares", "uShares")
@@ -229,7 +229,8 @@ def masked_input_to_json(ctx: _lib.Context, mi: MaskedInput) -> str:
     the {"value":"..."} records are framed with numpy (37 B per word)."""
     W = len(mi.data)
     if W:
-        words = np.frombuffer(b"".join(d.value for d in mi.data), np.uint8).reshape(W, 16)
+        words = mi.data.words if hasattr(mi.data, "words") else \
+            np.frombuffer(b"".join(d.value for d in mi.data), np.uint8).reshape(W, 16)
         rec = ctx.base64_encode_words(words)
         frame = np.empty((W, 37), np.uint8)
         frame[:, :10] = np.frombuffer(b'{"value":"', np.uint8)
@@ -242,7 +243,42 @@ def masked_input_to_json(ctx: _lib.Context, mi: MaskedInput) -> str:
     return '{"secretId":"%s","data":%s,"tags":%s}' % (mi.secret_id, data.decode("ascii"), tags)
 
 
+_RECORD = np.frombuffer(b'{"value":"', np.uint8)
+
+
+def _compact_records(text: str):
+    """The (W, 24) base64 records of a MaskedInput body in the compact layout
+    (what masked_input_to_json and Jackson's default writer produce:
+    "data":[{"value":"<24>"},...]) located without a JSON tree, plus the text
+    with the data array emptied; None for any other layout."""
+    k = text.find('"data":[')
+    if k < 0 or text.count('"data"') != 1:
+        return None
+    lb = k + len('"data":')
+    rb = text.find("]", lb)
+    if rb < 0:
+        return None
+    span = text[lb + 1:rb]
+    if not span:
+        return np.zeros((0, 24), np.uint8), text[:lb] + "[]" + text[rb + 1:]
+    if (len(span) + 1) % 37:
+        return None
+    b = np.frombuffer((span + ",").encode("ascii", errors="replace"), np.uint8).reshape(-1, 37)
+    if not (np.array_equal(b[:, :10], np.broadcast_to(_RECORD, (b.shape[0], 10)))
+            and (b[:, 34] == ord('"')).all() and (b[:, 35] == ord("}")).all() and (b[:, 36] == ord(",")).all()):
+        return None
+    return np.ascontiguousarray(b[:, 10:34]), text[:lb] + "[]" + text[rb + 1:]
+
+
 def masked_input_from_json(ctx: _lib.Context, text: str) -> MaskedInput:
+    fast = _compact_records(text)
+    if fast is not None:  # the records go to the GPU decoder as one array
+        rec, rest = fast
+        obj = json.loads(rest)
+        if obj.get("secretId") is None:
+            raise IllegalArgumentException("secretId is marked non-null but is null")
+        words = ctx.base64_decode_words(rec) if rec.shape[0] else np.zeros((0, 16), np.uint8)
+        return MaskedInput(uuid.UUID(obj["secretId"]), MaskedInputWords(words), list(obj.get("tags") or []))
     obj = json.loads(text)
     if obj.get("secretId") is None:
         raise IllegalArgumentException("secretId is marked non-null but is null")

@@ -5,7 +5,10 @@ JSON.  Reports the upload and download latencies; the fake Castor dealer
 (Python tuple generation, test infrastructure) generates each request's
 tuples before the timed call.
 
-    python tools/bench_c1.py [--words 1000] [--reps 20]
+    python tools/bench_c1.py [--words 1000] [--reps 20] [--transport objects|json]
+
+--transport json: the client-party hops carry the REST JSON bodies and the
+client runs K_RV / K_MASK straight from the base64 text.
 """
 import argparse
 import json
@@ -25,6 +28,7 @@ def main():
     ap.add_argument("--words", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--parties", type=int, default=2)
+    ap.add_argument("--transport", choices=["objects", "json"], default="objects")
     a = ap.parse_args()
     import amphora_amd as A
     from amphora_amd.loopback import AmphoraParty, ExchangeHub, LoopbackAmphoraClient
@@ -36,7 +40,7 @@ def main():
     castor = FakeCastor(P, R, RINV, keys, 1)
     hub = ExchangeHub(a.parties)
     parties = [AmphoraParty(j, P, R, RINV, keys[j], castor, hub) for j in range(a.parties)]
-    client = LoopbackAmphoraClient(parties, P, R, RINV)
+    client = LoopbackAmphoraClient(parties, P, R, RINV, transport=a.transport)
     data = [rng.randrange(2 ** 63) for _ in range(a.words)]
     W = a.words
     from amphora_amd import loopback as LB
@@ -72,12 +76,13 @@ def main():
             t2 = time.perf_counter()
         finally:
             LB.uuid.uuid4 = real_uuid4
-        assert got.data == data
+        assert [int(x) for x in got.data] == data
         if rep >= 2:
             up.append((t1 - t0) * 1e3)
             down.append((t2 - t1) * 1e3)
     client.close()
-    print(json.dumps({"config": "C1: %d-word upload+download, %d loopback parties, JSON opens" % (a.words, a.parties),
+    print(json.dumps({"config": "C1: %d-word upload+download, %d loopback parties, JSON opens, %s client-party hops"
+                                % (a.words, a.parties, a.transport),
                       "upload_ms_median": statistics.median(up), "download_ms_median": statistics.median(down),
                       "reps": a.reps, "note": "fake-Castor tuples generated before each timed call (test dealer, not the path)"}))
 
