@@ -521,16 +521,30 @@ __device__ __forceinline__ uint32_t dec_unit_slow(const char* t, size_t unit, si
 #endif
 constexpr int kWirePrefetch = AMPH_WIRE_PD;
 
+// Fields decoded per barrier (AMPH_WIRE_G): G units of text go to LDS before
+// each barrier (2G buffers alternate, or all 5N at once, one barrier in all,
+// when G >= 5N).
+#ifndef AMPH_WIRE_G
+#define AMPH_WIRE_G 5  // 2-5 % over 1 at 1 and 16 Mi words (profiles/r02_ubench_wire_groups.txt)
+#endif
+template <int NP>
+struct WireGroups {
+  static constexpr int F = 5 * (NP > 0 ? NP : 1);  // fields (runtime party counts: G = 1)
+  static constexpr int G = NP > 0 ? (AMPH_WIRE_G < F ? AMPH_WIRE_G : F) : 1;
+  static constexpr int bufs = G >= F ? F : 2 * G;
+};
+
 template <int NP, bool BIG, bool FAST, int BS>
 __device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nchars, uint32_t pad,
                                             size_t words, uint4 (&raw)[5][NP > 0 ? NP : 1],
                                             uint32_t (*lds)[3 * BS], W4 (&acc)[5],
                                             unsigned long long* bad, const Fp& f) {
+  constexpr int G = WireGroups<NP>::G, NB = WireGroups<NP>::bufs;
   const size_t unit = (size_t)blockIdx.x * BS + threadIdx.x;
   const size_t word = (size_t)blockIdx.x * Wire<BS>::words + threadIdx.x;
   const bool consumer = threadIdx.x < Wire<BS>::words && word < words;
   const int np = NP > 0 ? NP : n;
-  int buf = 0;
+  int slot = 0;  // LDS buffer of the next field
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
 #pragma unroll
@@ -552,17 +566,29 @@ __device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nch
       }
       if (fb != 0xFFFFFFFFu)  // (party j, field k) in ODO order, then the offset
         atomicMin(bad, (unsigned long long)((size_t)(5 * j + k) * nchars + 16 * unit + fb));
-      uint32_t* l = lds[buf];
+      uint32_t* l = lds[slot];
       l[3 * threadIdx.x] = o[0];
       l[3 * threadIdx.x + 1] = o[1];
       l[3 * threadIdx.x + 2] = o[2];
-      __syncthreads();
-      if (consumer) {
-        const uint4 v = reinterpret_cast<const uint4*>(l)[threadIdx.x];
-        const W4 x = canon<BIG>(w4(v), f);
-        acc[k] = j == 0 ? x : mod_add(acc[k], x, f);
+      const int fi = k * (NP > 0 ? NP : 1) + j;  // flat field index (G = 1 for runtime counts)
+      const bool group_end = G == 1 || (fi + 1) % G == 0 || fi + 1 == WireGroups<NP>::F;
+      if (group_end) {
+        __syncthreads();
+        if (consumer) {
+          // the group's fields, oldest first: fields fi - m, m = cnt-1 .. 0
+          const int cnt = G == 1 ? 1 : (fi % G) + 1;
+#pragma unroll
+          for (int m = (G == 1 ? 0 : G - 1); m >= 0; --m) {
+            if (m >= cnt) continue;
+            const int ff = fi - m, kk = G == 1 ? k : ff / (NP > 0 ? NP : 1), jj = G == 1 ? j : ff % (NP > 0 ? NP : 1);
+            const int sl = (slot - m + NB) % NB;
+            const uint4 v = reinterpret_cast<const uint4*>(lds[sl])[threadIdx.x];
+            const W4 x = canon<BIG>(w4(v), f);
+            acc[kk] = jj == 0 ? x : mod_add(acc[kk], x, f);
+          }
+        }
       }
-      buf ^= 1;
+      slot = (slot + 1) % NB;
     }
   }
 }
@@ -588,7 +614,7 @@ template <int NP, bool BIG, int BS>
 __global__ __launch_bounds__(BS) void k_rv_b64(TextSet tx, int n, size_t words, size_t nchars,
                                            uint32_t pad, uint4* out_y, unsigned long long* ff,
                                            unsigned long long* bad, Fp f) {
-  __shared__ uint32_t lds[2][3 * BS];
+  __shared__ uint32_t lds[WireGroups<NP>::bufs < 2 ? 2 : WireGroups<NP>::bufs][3 * BS];
   W4 acc[5];
   uint4 raw[5][NP > 0 ? NP : 1];
   const bool fast = ((size_t)blockIdx.x + 1) * Wire<BS>::chars + 4 <= nchars;
@@ -621,7 +647,7 @@ __global__ __launch_bounds__(BS) void k_mask_b64(TextSet tx, int n, size_t words
                                              uint4* out16, char* out24, unsigned long long* ff,
                                              unsigned long long* bad, Fp f) {
   constexpr int WW = Wire<BS>::words;
-  __shared__ uint32_t lds[2][3 * BS];
+  __shared__ uint32_t lds[WireGroups<NP>::bufs < 2 ? 2 : WireGroups<NP>::bufs][3 * BS];
   W4 acc[5];
   uint4 raw[5][NP > 0 ? NP : 1];
   const size_t word = (size_t)blockIdx.x * WW + threadIdx.x;
