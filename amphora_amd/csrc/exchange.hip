@@ -15,9 +15,10 @@
 // formats them into LDS and stores the contiguous run with aligned 16-byte
 // stores.
 //
-// Decode (array text -> diffs): every lane classifies 32 bytes; number starts
-// are counted per workgroup, scanned, and each start is parsed by the lane
-// that found it at its global number index.  Each number's key ("a" / "b"),
+// Decode (array text -> diffs): values are numbered by the colon before them
+// ("k":NUM).  Every lane counts the colons in its bytes; the counts are
+// scanned per workgroup, and the value after each colon is parsed at its
+// global number index.  Each number's key ("a" / "b"),
 // the object it sits in (member 0 after '{', member 1 after ','), the other
 // member's key and the closing '}' are checked locally, so the pairing is
 // validated without a second pass; the first malformed byte's offset is
@@ -385,59 +386,24 @@ __device__ __forceinline__ uint32_t swar_digit(uint32_t w) {
   const uint32_t lo = w & 0x7F7F7F7Fu;
   return (lo + 0x50505050u) & ~(lo + 0x46464646u) & ~w & 0x80808080u;  // 0x30 <= b <= 0x39
 }
-// Number-token byte classes of 4 text bytes by table lookup (v_perm_b32 as an
-// 8-entry byte table): class = HI[b >> 4] & LO[b & 15] with the bits
-//   1 '+' '-' '.' (high nibble 2, low nibble B / D / E)   2 '-' (start)
-//   4 digits (high nibble 3, low nibble 0-9)              8 'e' 'E' (high 6 / 4, low 5)
-// num: bit 7 of byte j set iff byte j continues a number token (digits, sign,
-// fraction, exponent); start: iff it may start one (digit or '-').  Bytes
-// >= 0x80 are in neither class.  19 VALU ops for both masks (bitwise compares
-// took ~40).
-__device__ __forceinline__ void num_classes(uint32_t w, uint32_t& num, uint32_t& start) {
-  const uint32_t lo = w & 0x0F0F0F0Fu, l7 = lo & 0x07070707u;
-  const uint32_t la = __builtin_amdgcn_perm(0x04040C04u, 0x04040404u, l7);  // LO[0..7]
-  const uint32_t lb = __builtin_amdgcn_perm(0x00010300u, 0x01000404u, l7);  // LO[8..15]
-  const uint32_t cl = __builtin_amdgcn_perm(lb, la, 0x03020100u | ((lo & 0x08080808u) >> 1));
-  const uint32_t ch = __builtin_amdgcn_perm(0x00080008u, 0x04030000u, (w >> 4) & 0x07070707u);
-  const uint32_t cls = ch & cl, ascii = ~w & 0x80808080u;
-  num = (cls + 0x7F7F7F7Fu) & ascii;
-  start = ((cls & 0x06060606u) + 0x7F7F7F7Fu) & ascii;
+// Colons in 4 text bytes: bit 7 of byte j set iff byte j is ':' (exact
+// zero-byte test of w ^ "::::").  Every number of a FactorPair list follows
+// exactly one colon ("k":NUM), so the decoder numbers the values by their
+// colons: counting them is 5 VALU ops per 4 bytes where the number-start
+// classes of the number tokens took 19, and a colon that is not followed by a number, or a number
+// without one, breaks the grammar checks around its neighbours.
+__device__ __forceinline__ uint32_t swar_colon(uint32_t w) {
+  const uint32_t x = w ^ 0x3A3A3A3Au;
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
 }
-__device__ __forceinline__ uint32_t swar_numchar(uint32_t w) {
-  uint32_t num, start;
-  num_classes(w, num, start);
-  return num;
-}
-
-// Number starts in 32 text bytes (8 dwords): a digit or '-' whose predecessor
-// does not continue a number.  prev_nc: numchar flag of the byte before (bit 31).
-// Returns one bit per byte.
-__device__ __forceinline__ uint32_t starts32(const uint32_t (&w)[8], uint32_t prev_nc) {
+__device__ __forceinline__ uint32_t colons32(const uint32_t (&w)[8]) {  // one bit per byte
   uint32_t m = 0;
 #pragma unroll
   for (int d = 0; d < 8; ++d) {
-    uint32_t nc, st;
-    num_classes(w[d], nc, st);
-    const uint32_t pnc = (nc << 8) | (prev_nc >> 24);
-    const uint32_t s = (st & ~pnc) >> 7;
-    m |= ((s | (s >> 7) | (s >> 14) | (s >> 21)) & 0xFu) << (4 * d);
-    prev_nc = nc;
+    const uint32_t c = swar_colon(w[d]) >> 7;
+    m |= ((c | (c >> 7) | (c >> 14) | (c >> 21)) & 0xFu) << (4 * d);
   }
   return m;
-}
-
-// The number of starts in 32 text bytes (what __popc(starts32(...)) gives,
-// without packing the per-byte flags into a bit mask).
-__device__ __forceinline__ uint32_t count_starts32(const uint32_t (&w)[8], uint32_t prev_nc) {
-  uint32_t n = 0;
-#pragma unroll
-  for (int d = 0; d < 8; ++d) {
-    uint32_t nc, st;
-    num_classes(w[d], nc, st);
-    n += __popc(st & ~((nc << 8) | (prev_nc >> 24)));
-    prev_nc = nc;
-  }
-  return n;
 }
 
 constexpr int kDecBlock = 256;  // threads per workgroup (512: parse 574 us, 256: 486, 128: 527 at 8 Mi pairs)
@@ -445,9 +411,9 @@ constexpr size_t kDecSpan = (size_t)kDecBlock * kDecBytes;  // 8 KiB of text per
 constexpr int kWinPad = 256;                           // window context either side
 constexpr int kWin = (int)kDecSpan + 2 * kWinPad;      // staged bytes
 
-// Pass 1: number starts per 8 KiB span.  128 lanes x 64 bytes (four 16-B
-// loads in flight per lane, nontemporal: the text is read once here and once
-// by the parse), a wave reduction and one LDS word per wave.
+// Pass 1: colons (= numbers) per 8 KiB span.  128 lanes x 64 bytes (four
+// 16-B loads in flight per lane, nontemporal: the text is read once here and
+// once by the parse), a wave reduction and one LDS word per wave.
 constexpr int kCntBlock = 128;
 constexpr int kCntBytes = (int)(kDecSpan / kCntBlock);  // 64
 static_assert(kCntBytes == 64, "count lanes read four 16-B chunks");
@@ -467,12 +433,11 @@ __global__ __launch_bounds__(kCntBlock) void k_xdec_count(Text t, uint64_t* bsum
 #pragma unroll
     for (int k = 0; k < 4; ++k) c[k] = t.chunk((long long)base + 16 * k);
   }
-  const uint32_t w0[8] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w};
-  const uint32_t w1[8] = {c[2].x, c[2].y, c[2].z, c[2].w, c[3].x, c[3].y, c[3].z, c[3].w};
-  // numchar flag of the byte before: the previous lane's last dword (lane 0: a load)
-  const uint32_t prev_last = __shfl_up(w1[7], 1, 64);
-  const uint32_t pb = __lane_id() == 0 ? (base ? t[base - 1] : (uint32_t)' ') << 24 : prev_last;
-  uint32_t cnt = count_starts32(w0, swar_numchar(pb)) + count_starts32(w1, swar_numchar(w0[7]));
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    cnt += __popc(swar_colon(c[k].x)) + __popc(swar_colon(c[k].y)) + __popc(swar_colon(c[k].z)) +
+           __popc(swar_colon(c[k].w));
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
   if (__lane_id() == 0) wsum[threadIdx.x >> 6] = cnt;
@@ -636,8 +601,8 @@ __device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, boo
   return !ovf;
 }
 
-// Pass 3: each workgroup finds its number starts again (from LDS), scans
-// them to global number indices and lists their positions in LDS; then its
+// Pass 3: each workgroup finds its colons again (from LDS), scans them to
+// global number indices and lists their positions in LDS; then its
 // lanes take ONE NUMBER EACH, consecutive numbers on consecutive lanes (so a
 // wave's trip counts match), read the digits four at a time (SWAR) and check
 // the grammar around the number:
@@ -649,7 +614,7 @@ __device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, boo
 // ties each member 1 to the member 0 before it (same ',', other key), so
 // together they cover every byte of a well-formed array.  A well-formed text
 // has at most kMaxStarts numbers per 8 KiB span ({"a":1,"b":2}, = 14 bytes per 2);
-// a start beyond that is reported as malformed.
+// a colon beyond that is reported as malformed.
 constexpr int kMaxStarts = 1280;
 
 __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint64_t* bscan,
@@ -669,7 +634,7 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint6
   const int lo = kWinPad + kDecBytes * threadIdx.x;  // this lane's 32 bytes in the window
   const uint4 c0 = win4[lo / 16], c1 = win4[lo / 16 + 1];
   const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-  uint32_t m = starts32(w, swar_numchar((uint32_t)win[lo - 1] << 24));
+  uint32_t m = colons32(w);  // this lane's colons: one value each
   uint64_t total;
   const uint64_t first = block_excl_scan(__popc(m), &total);
   for (int k = (int)first; m; m &= m - 1, ++k) {
@@ -683,10 +648,11 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint6
   // phase 1: own checks + value
   const uint32_t* l32 = reinterpret_cast<const uint32_t*>(win4);
   for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
-    const size_t x = b0 + pos[idx];
+    // the value's first byte: right after its colon, or after whitespace
+    size_t x = b0 + pos[idx] + 1;
     const uint64_t g = gbase + idx;
     const bool first_m = (g & 1) == 0;
-    if (g > 0 && g + 1 < nvals) {
+    if (g > 0 && g + 1 < nvals && !is_ws(win[x - (size_t)w0])) {
       FastNum fn;
       const uint32_t o = (uint32_t)(x - (size_t)w0);
       if (fast_number(l32, o, first_m, fn)) {
@@ -699,6 +665,7 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint6
         continue;
       }
     }
+    while (x < text.L && is_ws(t[x])) ++x;
     size_t q = 0;
     const uint32_t key = key_before(t, x, &q);
     bool ok = key != 0 && g < nvals && q > 0;
@@ -775,7 +742,8 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint6
     if (idx > 0) {
       ok = comma[idx] == endp[idx - 1] && keyc[idx - 1] != 0 && keyc[idx - 1] != key;
     } else {  // member 0 sits in the previous span: walk back over its digits
-      const size_t x = b0 + pos[idx];
+      size_t x = b0 + pos[idx] + 1;
+      while (x < text.L && is_ws(t[x])) ++x;
       size_t q = 0;
       key_before(t, x, &q);
       size_t r = skip_ws_back(t, q - 1);
@@ -785,7 +753,11 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint6
       const uint32_t k0 = key_before(t, r, &q0);
       ok = k0 != 0 && k0 != key && q0 > 0 && t[q0 - 1] == '{';
     }
-    if (!ok) atomicMin(bad, (unsigned long long)(b0 + pos[idx] - text.mis));
+    if (!ok) {
+      size_t x = b0 + pos[idx] + 1;
+      while (x < text.L && is_ws(t[x])) ++x;
+      atomicMin(bad, (unsigned long long)(x - text.mis));
+    }
   }
 }
 
