@@ -411,43 +411,37 @@ constexpr size_t kDecSpan = (size_t)kDecBlock * kDecBytes;  // 8 KiB of text per
 constexpr int kWinPad = 256;                           // window context either side
 constexpr int kWin = (int)kDecSpan + 2 * kWinPad;      // staged bytes
 
-// Pass 1: colons (= numbers) per 8 KiB span.  128 lanes x 64 bytes (four
-// 16-B loads in flight per lane, nontemporal: the text is read once here and
-// once by the parse), a wave reduction and one LDS word per wave.
-constexpr int kCntBlock = 128;
-constexpr int kCntBytes = (int)(kDecSpan / kCntBlock);  // 64
-static_assert(kCntBytes == 64, "count lanes read four 16-B chunks");
+// Pass 1: colons (= numbers) per 8 KiB span, ONE WAVE PER SPAN: 64 lanes x
+// eight 16-B loads in flight, lane-interleaved so that every wave
+// instruction reads 1 KiB contiguous (nontemporal: the text is read once here
+// and once by the parse), a wave reduction, no LDS or barrier; four spans per
+// 256-lane workgroup.  96 us per 640 MB text where 128 lanes x 64
+// lane-contiguous bytes per span took 162 (tools/ubench/ubench_xcount.hip).
+constexpr int kCntWaves = 4;
 
-__global__ __launch_bounds__(kCntBlock) void k_xdec_count(Text t, uint64_t* bsum) {
-  __shared__ uint32_t wsum[kCntBlock / 64];
-  const size_t base = (size_t)blockIdx.x * kDecSpan + (size_t)threadIdx.x * kCntBytes;
-  uint4 c[4];
-  if (base >= t.mis && base + kCntBytes <= t.L) {
-    const u32x4* p = reinterpret_cast<const u32x4*>(t.al + base);
+__global__ __launch_bounds__(64 * kCntWaves) void k_xdec_count(Text t, uint64_t* bsum, size_t nb) {
+  const size_t span = (size_t)blockIdx.x * kCntWaves + (threadIdx.x >> 6);
+  if (span >= nb) return;
+  const size_t base = span * kDecSpan + (size_t)(threadIdx.x & 63) * 16;
+  uint4 c[8];
+  if (span * kDecSpan >= t.mis && (span + 1) * kDecSpan <= t.L) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const u32x4 v = __builtin_nontemporal_load(p + k);
+    for (int k = 0; k < 8; ++k) {
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t.al + base + 1024 * k));
       c[k] = make_uint4(v.x, v.y, v.z, v.w);
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) c[k] = t.chunk((long long)base + 16 * k);
+    for (int k = 0; k < 8; ++k) c[k] = t.chunk((long long)(base + 1024 * k));
   }
   uint32_t cnt = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < 8; ++k)
     cnt += __popc(swar_colon(c[k].x)) + __popc(swar_colon(c[k].y)) + __popc(swar_colon(c[k].z)) +
            __popc(swar_colon(c[k].w));
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-  if (__lane_id() == 0) wsum[threadIdx.x >> 6] = cnt;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t total = 0;
-#pragma unroll
-    for (int k = 0; k < kCntBlock / 64; ++k) total += wsum[k];
-    bsum[blockIdx.x] = total;
-  }
+  if ((threadIdx.x & 63) == 0) bsum[span] = cnt;
 }
 
 // The workgroup's 8 KiB span plus kWinPad bytes either side, staged in LDS;
@@ -853,7 +847,7 @@ hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, u
   c0.ev_stop = nullptr;
   cm.ev_start = cm.ev_stop = nullptr;
   c1.ev_start = nullptr;
-  AMPH_LAUNCH(k_xdec_count, dim3((unsigned)nb), dim3(kCntBlock), c0, t, bscan);
+  AMPH_LAUNCH(k_xdec_count, dim3(blocks_of(nb, kCntWaves)), dim3(64 * kCntWaves), c0, t, bscan, nb);
   hipError_t e = scan_u64(bscan, nb, bsum, cm);
   if (e != hipSuccess) return e;
   AMPH_LAUNCH(k_xdec_parse, dim3((unsigned)nb), dim3(kDecBlock), cm, t, bscan, 2 * npairs, mag, neg, bad);
