@@ -418,8 +418,16 @@ constexpr int kWin = (int)kDecSpan + 2 * kWinPad;      // staged bytes
 // 256-lane workgroup.  96 us per 640 MB text where 128 lanes x 64
 // lane-contiguous bytes per span took 162 (tools/ubench/ubench_xcount.hip).
 constexpr int kCntWaves = 4;
+// bsum / bscan words: colon count in bits 0..39, spans with whitespace from bit 40
+constexpr uint64_t kWsBit = 1ull << 40, kCountMask = kWsBit - 1;
 
-__global__ __launch_bounds__(64 * kCntWaves) void k_xdec_count(Text t, uint64_t* bsum, size_t nb) {
+__device__ __forceinline__ uint32_t swar_below21(uint32_t w) {  // nonzero iff some byte < 0x21
+  return (w - 0x21212121u) & ~w & 0x80808080u;
+}
+
+__global__ __launch_bounds__(64 * kCntWaves) void k_xdec_count(Text t, uint64_t* bsum, size_t nb,
+                                                             unsigned int* slow) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *slow = 0;  // k_xdec_fast's flag
   const size_t span = (size_t)blockIdx.x * kCntWaves + (threadIdx.x >> 6);
   if (span >= nb) return;
   const size_t base = span * kDecSpan + (size_t)(threadIdx.x & 63) * 16;
@@ -434,14 +442,19 @@ __global__ __launch_bounds__(64 * kCntWaves) void k_xdec_count(Text t, uint64_t*
 #pragma unroll
     for (int k = 0; k < 8; ++k) c[k] = t.chunk((long long)(base + 1024 * k));
   }
-  uint32_t cnt = 0;
+  uint32_t cnt = 0, low = 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k)
+  for (int k = 0; k < 8; ++k) {
     cnt += __popc(swar_colon(c[k].x)) + __popc(swar_colon(c[k].y)) + __popc(swar_colon(c[k].z)) +
            __popc(swar_colon(c[k].w));
+    low |= swar_below21(c[k].x) | swar_below21(c[k].y) | swar_below21(c[k].z) | swar_below21(c[k].w);
+  }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-  if ((threadIdx.x & 63) == 0) bsum[span] = cnt;
+  // whitespace (or a control byte) in a span wholly inside the text: the
+  // compact fast pass cannot hold, so it is skipped (kWsBit, summed by the scan)
+  const bool ws = span * kDecSpan >= t.mis && (span + 1) * kDecSpan <= t.L && __ballot(low != 0) != 0;
+  if ((threadIdx.x & 63) == 0) bsum[span] = cnt | (ws ? kWsBit : 0);
 }
 
 // The workgroup's 8 KiB span plus kWinPad bytes either side, staged in LDS;
@@ -536,6 +549,65 @@ __device__ __forceinline__ uint32_t lds_dword(const uint32_t* l32, uint32_t o) {
   return __builtin_amdgcn_alignbyte(l32[(o >> 2) + 1], l32[o >> 2], o & 3u);
 }
 
+// The number at window offset o: '-'? then 1..39 digits without a leading
+// zero, value < 2^128, followed by what after_ok(one past its last digit)
+// accepts (sets r.v, r.minus, r.dend; ok: the caller's own checks so far).
+// The digit run is found with SWAR over 44 bytes held in registers; the
+// value is folded in base 10^8 from the same registers: full 8-digit
+// chunks, then the nd % 8 leading digits of the next chunk right-aligned
+// behind '0's.
+template <class AfterOk>
+__device__ __forceinline__ bool fast_parse(const uint32_t* l32, uint32_t o, bool ok, FastNum& r,
+                                           AfterOk after_ok) {
+  const uint32_t first = lds_dword(l32, o);
+  r.minus = (first & 0xFFu) == (uint32_t)'-';
+  const uint32_t ds = o + (r.minus ? 1u : 0u);
+  uint32_t d[11];
+#pragma unroll
+  for (int j = 0; j < 11; ++j) d[j] = lds_dword(l32, ds + 4 * j);
+  uint32_t nd = 44;
+#pragma unroll
+  for (int j = 10; j >= 0; --j) {
+    const uint32_t x = d[j] ^ 0x30303030u;  // digits -> 0..9
+    const uint32_t nondig = (((x & 0x7F7F7F7Fu) + 0x76767676u) | x) & 0x80808080u;
+    if (nondig) nd = 4 * j + (__builtin_ctz(nondig) >> 3);
+  }
+  ok = ok && nd >= 1 && nd <= 39 && !((d[0] & 0xFFu) == (uint32_t)'0' && nd > 1);
+  if (!ok) return false;
+  r.dend = ds + nd;
+  if (!after_ok(r.dend)) return false;
+  const uint32_t full = nd >> 3, rem = nd & 7u;
+  bool ovf = false;
+  if (full == 4) {  // 32..39 digits (a random 128-bit value): two 16-digit halves
+    const uint64_t p0 = (uint64_t)digits8(d[0], d[1]) * 100000000u + digits8(d[2], d[3]);
+    const uint64_t p1 = (uint64_t)digits8(d[4], d[5]) * 100000000u + digits8(d[6], d[7]);
+    const unsigned __int128 t = (unsigned __int128)p0 * 10000000000000000ull + p1;  // < 10^32
+    r.v[0] = (uint32_t)t;
+    r.v[1] = (uint32_t)(t >> 32);
+    r.v[2] = (uint32_t)(t >> 64);
+    r.v[3] = (uint32_t)(t >> 96);
+  } else {
+    r.v[0] = r.v[1] = r.v[2] = r.v[3] = 0;
+#pragma unroll
+    for (uint32_t m = 0; m < 4; ++m)
+      if (m < full) fold(r.v, 100000000u, digits8(d[2 * m], d[2 * m + 1]), ovf);
+  }
+  if (rem) {
+    uint32_t lo = d[0], hi = d[1];
+#pragma unroll
+    for (uint32_t m = 1; m < 5; ++m)
+      if (m == full) { lo = d[2 * m]; hi = d[2 * m + 1]; }
+    const uint64_t x = ((uint64_t)hi << 32) | lo;
+    const uint32_t sh = 8 * (8 - rem);  // 8..56
+    const uint64_t y = (x << sh) | (0x3030303030303030ull >> (64 - sh));
+    fold(r.v, pow10_small(rem), digits8((uint32_t)y, (uint32_t)(y >> 32)), ovf);
+  }
+  return !ovf;
+}
+
+// The general pass's fast path (checks the context BEFORE the number; the
+// digit scan and conversion as fast_parse, kept separate: inlined through
+// fast_parse's lambda it cost the general kernel 20 bytes of scratch).
 __device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, bool member0,
                                             FastNum& r) {
   const uint32_t pre0 = lds_dword(l32, o - 8), pre1 = lds_dword(l32, o - 4);
@@ -595,7 +667,40 @@ __device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, boo
   return !ovf;
 }
 
-// Pass 3: each workgroup finds its colons again (from LDS), scans them to
+// Value g's SEGMENT in the compact layout, from the byte after its colon to
+// the next value's colon:
+//   NUM ',' '"' K '"' ':'            member 0 (K the other key)
+//   NUM '}' ',' '{' '"' K '"' ':'    member 1
+//   NUM '}' ']' <end of text>        the last value
+// plus its own key ('"' k '"' before the colon; value 0: the text starts
+// '[' '{' '"' k '"' ':').  The segments of all values tile the text from
+// its first byte to its last, so when every value's segment holds, the
+// whole array is well-formed; no neighbour's record is needed.
+// xo: absolute text offset of window offset o; len: the text length.
+__device__ __forceinline__ bool fast_segment(const uint32_t* l32, uint32_t o, uint64_t g,
+                                             size_t nvals, size_t xo, size_t len, FastNum& r) {
+  const uint32_t pre = lds_dword(l32, o - 4);
+  r.key = (pre >> 8) & 0xFFu;
+  bool ok = (pre & 0xFFFF00FFu) == 0x3A220022u && (r.key == 'a' || r.key == 'b');
+  if (g == 0) ok = ok && xo == 6 && (lds_dword(l32, o - 6) & 0xFFFFu) == 0x7B5Bu;  // "[{"
+  const uint32_t key = r.key;
+  return fast_parse(l32, o, ok, r, [=](uint32_t dend) {
+    const uint32_t a0 = lds_dword(l32, dend), a1 = lds_dword(l32, dend + 4);
+    if ((g & 1) == 0) {
+      const uint32_t k = (a0 >> 16) & 0xFFu;
+      return (a0 & 0xFF00FFFFu) == 0x2200222Cu && (k == 'a' || k == 'b') && k != key &&
+             (a1 & 0xFFu) == (uint32_t)':';
+    }
+    if (g + 1 == nvals) return (a0 & 0xFFFFu) == 0x5D7Du && xo + (dend - o) + 2 == len;  // "}]"
+    const uint32_t k = a1 & 0xFFu;
+    return a0 == 0x227B2C7Du && (a1 & 0x00FFFF00u) == 0x003A2200u && (k == 'a' || k == 'b');
+  });
+}
+
+// Pass 3, general (k_xdec_slow, one workgroup per span; its workgroups
+// return at once unless k_xdec_fast found a value outside the compact
+// layout): each
+// workgroup finds its colons again (from LDS), scans them to
 // global number indices and lists their positions in LDS; then its
 // lanes take ONE NUMBER EACH, consecutive numbers on consecutive lanes (so a
 // wave's trip counts match), read the digits four at a time (SWAR) and check
@@ -611,15 +716,18 @@ __device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, boo
 // a colon beyond that is reported as malformed.
 constexpr int kMaxStarts = 1280;
 
-__global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint64_t* bscan,
-                                                      size_t nvals, uint4* mag, uint8_t* neg,
-                                                      unsigned long long* bad) {
+__global__ __launch_bounds__(kDecBlock) void k_xdec_slow(Text text, const uint64_t* bscan, size_t nb,
+                                                     size_t nvals, uint4* mag, uint8_t* neg,
+                                                     unsigned long long* bad,
+                                                     const unsigned int* slow) {
+  if (*slow == 0 && (bscan[nb] & ~kCountMask) == 0) return;  // k_xdec_fast held (~13 us for 78 k spans)
   __shared__ uint4 win4[kWin / 16 + 1];
   __shared__ uint16_t pos[kMaxStarts];   // start, relative to b0
   __shared__ uint16_t endp[kMaxStarts];  // one past the last digit, relative to w0
   __shared__ uint16_t comma[kMaxStarts]; // member 1: one past the last byte before its ',', rel. w0
   __shared__ uint8_t keyc[kMaxStarts];   // 'a' / 'b', 0 if the number failed its own checks
-  const size_t b0 = (size_t)blockIdx.x * kDecSpan;
+  const size_t span = blockIdx.x;
+  const size_t b0 = span * kDecSpan;
   const long long w0 = (long long)b0 - kWinPad;
   for (int c = threadIdx.x; c < kWin / 16 + 1; c += kDecBlock) win4[c] = text.chunk(w0 + 16LL * c);
   __syncthreads();
@@ -638,7 +746,7 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint6
   }
   __syncthreads();
   const uint32_t nloc = (uint32_t)min(total, (uint64_t)kMaxStarts);
-  const uint64_t gbase = bscan[blockIdx.x];
+  const uint64_t gbase = bscan[span] & kCountMask;
   // phase 1: own checks + value
   const uint32_t* l32 = reinterpret_cast<const uint32_t*>(win4);
   for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
@@ -651,7 +759,9 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint6
       const uint32_t o = (uint32_t)(x - (size_t)w0);
       if (fast_number(l32, o, first_m, fn)) {
         endp[idx] = (uint16_t)fn.dend;
-        comma[idx] = (uint16_t)(o - 5);  // member 1: one past the byte before its ','
+        // one past the digit before this member's ',' (member 1) or before the '}'
+        // that closes the previous pair (member 0)
+        comma[idx] = (uint16_t)(first_m ? o - 7 : o - 5);
         keyc[idx] = (uint8_t)fn.key;
         const size_t slot = (g & ~(uint64_t)1) + (fn.key == 'b');
         mag[slot] = make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]);
@@ -675,6 +785,7 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint6
         ok = ok && r2 > 0 && t[r2 - 1] == '}';
         const size_t r3 = ok ? skip_ws_back(t, r2 - 1) : 0;
         ok = ok && r3 > 0 && is_digit(t[r3 - 1]);
+        cm = r3;
       }
     } else if (ok) {  // ',' ws before the key
       ok = t[q - 1] == ',';
@@ -727,25 +838,32 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint6
     neg[slot] = minus && (v[0] | v[1] | v[2] | v[3]) != 0;
   }
   __syncthreads();
-  // phase 2: member 1 follows its member 0: the same ',', the other key
+  // phase 2: every value follows the one before it: member 1's ',' and
+  // member 0's '}' sit right after the previous value's digits (ws aside),
+  // and member 1's key is not its member 0's
   for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
     const uint64_t g = gbase + idx;
     const uint32_t key = keyc[idx];
-    if ((g & 1) == 0 || key == 0) continue;
+    if (g == 0 || key == 0) continue;
+    const bool m1 = (g & 1) != 0;
     bool ok;
     if (idx > 0) {
-      ok = comma[idx] == endp[idx - 1] && keyc[idx - 1] != 0 && keyc[idx - 1] != key;
-    } else {  // member 0 sits in the previous span: walk back over its digits
+      ok = comma[idx] == endp[idx - 1] && keyc[idx - 1] != 0 && (!m1 || keyc[idx - 1] != key);
+    } else {  // the previous value sits in the previous span: walk back over its digits
       size_t x = b0 + pos[idx] + 1;
       while (x < text.L && is_ws(t[x])) ++x;
       size_t q = 0;
       key_before(t, x, &q);
-      size_t r = skip_ws_back(t, q - 1);
+      size_t r = skip_ws_back(t, q - 1);  // member 1: the ','; member 0: the '{'
+      if (!m1) {  // '{' ws ',' ws '}' ws <digit> (checked in phase 1)
+        r = skip_ws_back(t, r - 1);
+        r = skip_ws_back(t, r - 1);
+      }
       while (r > 0 && is_digit(t[r - 1])) --r;
       if (r > 0 && t[r - 1] == '-') --r;
       size_t q0 = 0;
       const uint32_t k0 = key_before(t, r, &q0);
-      ok = k0 != 0 && k0 != key && q0 > 0 && t[q0 - 1] == '{';
+      ok = k0 != 0 && (!m1 || (k0 != key && q0 > 0 && t[q0 - 1] == '{'));
     }
     if (!ok) {
       size_t x = b0 + pos[idx] + 1;
@@ -753,6 +871,54 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_parse(Text text, const uint6
       atomicMin(bad, (unsigned long long)(x - text.mis));
     }
   }
+}
+
+// Pass 3 (optimistic): the same staging and colon listing, then one value
+// per lane checked against its compact-layout SEGMENT (fast_segment) and
+// written; no whitespace walks, no records, no second phase, no general
+// path in the kernel (its registers cost occupancy: 100 SGPRs with it, 72
+// without).  Any value outside the compact layout (whitespace, a malformed
+// byte, value 0 or the last value not in the plain form, more colons than
+// expected) raises *slow, and k_xdec_slow then parses the whole text with
+// the general grammar and reports errors; Jackson's compact output never
+// takes it.
+__global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64_t* bscan, size_t nb,
+                                                     size_t nvals, uint4* mag, uint8_t* neg,
+                                                     unsigned int* slow) {
+  if ((bscan[nb] & ~kCountMask) != 0) return;  // whitespace somewhere: the general pass does it all
+  __shared__ uint4 win4[kWin / 16 + 1];
+  __shared__ uint16_t pos[kMaxStarts];  // colon, relative to b0
+  const size_t b0 = (size_t)blockIdx.x * kDecSpan;
+  const long long w0 = (long long)b0 - kWinPad;
+  for (int c = threadIdx.x; c < kWin / 16 + 1; c += kDecBlock) win4[c] = text.chunk(w0 + 16LL * c);
+  __syncthreads();
+  const int lo = kWinPad + kDecBytes * threadIdx.x;
+  const uint4 c0 = win4[lo / 16], c1 = win4[lo / 16 + 1];
+  const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  uint32_t m = colons32(w);
+  uint64_t total;
+  const uint64_t first = block_excl_scan(__popc(m), &total);
+  for (int k = (int)first; m && k < kMaxStarts; m &= m - 1, ++k)
+    pos[k] = (uint16_t)(kDecBytes * threadIdx.x + __ffs(m) - 1);
+  __syncthreads();
+  bool fail = total > (uint64_t)kMaxStarts;
+  const uint32_t nloc = (uint32_t)min(total, (uint64_t)kMaxStarts);
+  const uint64_t gbase = bscan[blockIdx.x] & kCountMask;
+  const uint32_t* l32 = reinterpret_cast<const uint32_t*>(win4);
+  const size_t len = text.L - text.mis;
+  for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
+    const uint32_t at = pos[idx];
+    const uint64_t g = gbase + idx;
+    FastNum fn;
+    if (g < nvals && fast_segment(l32, at + 1 + kWinPad, g, nvals, b0 + at + 1 - text.mis, len, fn)) {
+      const size_t slot = (g & ~(uint64_t)1) + (fn.key == 'b');
+      mag[slot] = make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]);
+      neg[slot] = fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0;
+    } else {
+      fail = true;
+    }
+  }
+  if (__ballot(fail) != 0 && __lane_id() == 0) atomicOr(slow, 1u);
 }
 
 // The array holds exactly nvals numbers and is bracketed; an empty array
@@ -767,7 +933,7 @@ __global__ __launch_bounds__(256) void k_xdec_check(Text t, const uint64_t* bsca
     while (z > t.mis && is_ws(t[z - 1])) --z;
     if (a >= t.L || t[a] != '[') atomicMin(bad, (unsigned long long)(a - t.mis));
     else if (z <= a + 1 || t[z - 1] != ']') atomicMin(bad, (unsigned long long)(z > t.mis ? z - 1 - t.mis : 0));
-    else if (bscan[nb] != nvals) atomicMin(bad, (unsigned long long)(t.L - t.mis));
+    else if ((bscan[nb] & kCountMask) != nvals) atomicMin(bad, (unsigned long long)(t.L - t.mis));
     az[0] = a + 1;
     az[1] = z > t.mis ? z - 1 : t.mis;
   }
@@ -830,10 +996,11 @@ hipError_t launch_exchange_encode(const uint4* mag, const uint8_t* neg, size_t n
   return hipGetLastError();
 }
 
-size_t xdec_scratch_bytes(size_t len) {
+size_t xdec_scratch_bytes(size_t len) {  // span counts, scan partials, the slow-path flag
   const size_t nb = blocks_of(len + 16, kDecSpan);
-  return 8 * (nb + 1) + 8 * ((size_t)blocks_of(nb, kScanBlock) + 1);
+  return 8 * (nb + 1) + 8 * ((size_t)blocks_of(nb, kScanBlock) + 1) + 8;
 }
+
 
 hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, uint4* mag,
                                   uint8_t* neg, unsigned long long* bad, void* scratch,
@@ -843,14 +1010,18 @@ hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, u
   const size_t nb = blocks_of(t.L ? t.L : 1, kDecSpan);
   uint64_t* bscan = static_cast<uint64_t*>(scratch);
   uint64_t* bsum = bscan + nb + 1;
+  unsigned int* slow = reinterpret_cast<unsigned int*>(bsum + blocks_of(nb, kScanBlock) + 1);
   LaunchCfg c0 = c, cm = c, c1 = c;
   c0.ev_stop = nullptr;
   cm.ev_start = cm.ev_stop = nullptr;
   c1.ev_start = nullptr;
-  AMPH_LAUNCH(k_xdec_count, dim3(blocks_of(nb, kCntWaves)), dim3(64 * kCntWaves), c0, t, bscan, nb);
+  AMPH_LAUNCH(k_xdec_count, dim3(blocks_of(nb, kCntWaves)), dim3(64 * kCntWaves), c0, t, bscan, nb, slow);
   hipError_t e = scan_u64(bscan, nb, bsum, cm);
   if (e != hipSuccess) return e;
-  AMPH_LAUNCH(k_xdec_parse, dim3((unsigned)nb), dim3(kDecBlock), cm, t, bscan, 2 * npairs, mag, neg, bad);
+  AMPH_LAUNCH(k_xdec_fast, dim3((unsigned)nb), dim3(kDecBlock), cm, t, bscan, nb, 2 * npairs, mag, neg,
+              slow);
+  AMPH_LAUNCH(k_xdec_slow, dim3((unsigned)nb), dim3(kDecBlock), cm, t, bscan, nb, 2 * npairs, mag,
+              neg, bad, (const unsigned int*)slow);
   AMPH_LAUNCH(k_xdec_check, dim3(1), dim3(256), c1, t, bscan, nb, 2 * npairs, bad);
   return hipGetLastError();
 }

@@ -352,6 +352,8 @@ def test_exchange_decode_rejects(ctx, text, where):
     (b'{"a":340282366920938463463374607431768211456,"b":2}', 20),
     (b'{"a":--1,"b":2}', 20), (b'{"a":01,"b":2}', 20), (b'{"a":-00,"b":2}', 20),
     (b'{"a":1,"b":-}', 26), (b'{"a":1,"b":2 }', 26), (b'{"a": 1,"b":2}', 21),
+    (b'{"a":1,7,"b":2}', 28),    # a stray value between the members: reported at member 1
+    (b'{"a":1,"b":2}5}', 36),    # stray bytes after a pair: reported at the next member 0
 ])
 def test_exchange_decode_rejects_mid_array(ctx, middle, where):
     """The same defects in a pair that is neither first nor last, among
@@ -385,6 +387,33 @@ def test_exchange_decode_rejects_edges(ctx, text, npairs, where):
         json.loads(text)
     with pytest.raises(ValueError, match="offset %d$" % where):
         ctx.exchange_decode(text, npairs)
+
+
+def test_exchange_decode_stray_bytes_between_pairs(ctx):
+    """'...,"b":4}5},{"a":6,...': the digit before the '}' that member 0
+    sees is not the previous value's, so the values around it are tied: the
+    previous value's digits must end right at that '}'.  Reported at the next
+    member 0, including where the two values fall in different 8 KiB decode
+    spans (the tie then walks back into the previous span)."""
+    pairs = _random_pairs(3000, 11)
+    items = ['{"a":%d,"b":%d}' % p for p in pairs]
+    ends, start = [], 1  # start: offset of item k
+    for k in range(len(items) - 1):
+        where = start + len(items[k]) + len('5},{"a":')  # the next member 0's number
+        ycolon = start + len('{"a":%d,"b":' % pairs[k][0]) - 1  # the previous value's colon
+        ends.append((k, where, ycolon))
+        start += len(items[k]) + 1
+    crossing = [(k, w) for k, w, y in ends if (w - 1) // 8192 != y // 8192][:4]
+    ends = [(k, w) for k, w, y in ends]
+    assert len(crossing) >= 2
+    for k, where in crossing + [(0, ends[0][1]), (1500, ends[1500][1]), ends[-1]]:
+        bad_items = list(items)
+        bad_items[k] += "5}"
+        text = ("[" + ",".join(bad_items) + "]").encode()
+        with pytest.raises(ValueError):
+            json.loads(text)
+        with pytest.raises(ValueError, match="offset %d$" % where):
+            ctx.exchange_decode(text, len(pairs))
 
 
 def test_exchange_decode_block_boundaries(ctx):
