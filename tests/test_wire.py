@@ -416,6 +416,68 @@ def test_exchange_decode_stray_bytes_between_pairs(ctx):
             ctx.exchange_decode(text, len(pairs))
 
 
+def _factor_pairs_or_none(text: bytes, npairs: int):
+    """The grammar oracle for the mutation test: Python's json module (any
+    JSON whitespace, no trailing data) plus the FactorPair shape -- exactly
+    the two members "a" and "b" per object, integer values below 2^128 in
+    magnitude, npairs objects.  Returns the (a, b) list or None."""
+    try:
+        items = json.loads(text, object_pairs_hook=lambda kv: ("obj", kv))
+    except (ValueError, UnicodeDecodeError):
+        return None
+    if not isinstance(items, list) or len(items) != npairs:
+        return None
+    out = []
+    for it in items:
+        if not (isinstance(it, tuple) and it[0] == "obj"):
+            return None
+        kv = it[1]
+        if sorted(k for k, _ in kv) != ["a", "b"]:
+            return None
+        if any(type(v) is not int or abs(v) >= 2 ** 128 for _, v in kv):
+            return None
+        d = dict(kv)
+        out.append((d["a"], d["b"]))
+    return out
+
+
+@pytest.mark.parametrize("npairs,seed,cases", [(40, 3, 2000), (700, 4, 400)])
+def test_exchange_decode_mutations(ctx, npairs, seed, cases):
+    """Single-byte replacements, insertions and deletions anywhere in a
+    compact FactorPair array (one decode span, and several): the decoder
+    accepts exactly the texts the grammar oracle accepts -- whichever of its
+    passes (compact or general) takes them -- and decodes them to the
+    oracle's values."""
+    rng = random.Random(seed)
+    pairs = _random_pairs(npairs, seed)
+    base = json.dumps([{"a": a, "b": b} for a, b in pairs], separators=(",", ":")).encode()
+    alphabet = b'{}[],:"ab-0123456789 x\n'
+    accepted = rejected = 0
+    for _ in range(cases):
+        t = bytearray(base)
+        i = rng.randrange(len(t) + 1)
+        op = rng.randrange(3)
+        c = alphabet[rng.randrange(len(alphabet))]
+        if op == 0 and i < len(t):
+            t[i] = c
+        elif op == 1:
+            t.insert(i, c)
+        elif i < len(t):
+            del t[i]
+        text = bytes(t)
+        want = _factor_pairs_or_none(text, npairs)
+        if want is None:
+            with pytest.raises(ValueError):
+                ctx.exchange_decode(text, npairs)
+            rejected += 1
+        else:
+            mag, neg = ctx.exchange_decode(text, npairs)
+            exp_m, exp_n = _diff_arrays(want)
+            assert np.array_equal(mag, exp_m) and np.array_equal(neg, exp_n), text[max(0, i - 20):i + 20]
+            accepted += 1
+    assert accepted > cases // 10 and rejected > cases // 3
+
+
 def test_exchange_decode_block_boundaries(ctx):
     """Numbers and their keys straddling the 16 KiB workgroup spans, long
     whitespace runs longer than the staged window, "-0" and zeros."""
