@@ -110,6 +110,56 @@ def test_rv_b64_bad_characters(ctx, F, mode, W):
     assert bad == (5 * 1 + 4) * nchars + 20
 
 
+_B64 = frozenset(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/")
+
+
+def _first_bad(t: bytes, pad: int) -> int:
+    """Offset of the first character Jackson's MIME_NO_LINEFEEDS decoder
+    rejects: outside the alphabet before the padding, anything but '=' in
+    it; -1 if none."""
+    body = len(t) - pad
+    for i, c in enumerate(t):
+        if (c not in _B64) if i < body else (c != ord("=")):
+            return i
+    return -1
+
+
+@pytest.mark.parametrize("W", [64, 65, 66])  # padding '==' / '=' / ''
+def test_rv_b64_mutations(ctx, F, W):
+    """Random single-character replacements in a random party's random field:
+    an invalid character is reported at its (5 party + field) nchars +
+    offset; a valid one changes the decoded word (Python's base64 says how),
+    and the verdict and secrets equal the C oracle's on those words."""
+    import random
+    rng = random.Random(W)
+    n = 2
+    odos, _ = F.synth_odos(seed=1200 + W, n=n, W=W)
+    base = texts_of(odos)
+    nchars = len(base[0][0])
+    pad = (3 - (16 * W) % 3) % 3
+    alphabet = sorted(_B64)
+    for _ in range(150):
+        j, k, pos = rng.randrange(n), rng.randrange(5), rng.randrange(nchars)
+        r = rng.random()
+        ch = alphabet[rng.randrange(64)] if r < 0.5 else ord("=") if r < 0.7 else rng.randrange(256)
+        t = bytearray(base[j][k])
+        t[pos] = ch
+        texts = [list(o) for o in base]
+        texts[j][k] = bytes(t)
+        y, ff, bad = _rv(ctx, texts, W, "device")
+        fb = _first_bad(bytes(t), pad)
+        if fb >= 0:
+            assert bad == (5 * j + k) * nchars + fb, (j, k, pos, ch)
+            continue
+        assert bad == -1, (j, k, pos, ch)
+        words = [list(o) for o in odos]
+        words[j][k] = np.frombuffer(base64.b64decode(bytes(t), validate=True), np.uint8).reshape(W, 16)
+        oy, off = F.recombine_verify([tuple(o) for o in words])
+        assert ff == off, (j, k, pos, ch)
+        if off < 0:
+            assert np.array_equal(y, oy)
+
+
 def test_rv_b64_length_checks(ctx, F):
     import amphora_amd as A
     odos, _ = F.synth_odos(seed=950, n=2, W=100)
