@@ -194,14 +194,19 @@ def scatter_mode(a, A, torch, dist, ctx, rank, world):
                          "words_total": W, "parties": n, "parallelism": "dp%d" % world}})
 
 
-def host_mode(a, A, torch, ctx):
-    """End-to-end host-memory rate (SURVEY.md C5 per GPU): ODOs and secrets
-    live in (pageable or page-locked) host memory; each step streams them
-    through the GPU in --batch-words batches (3-slot HtoD/compute/DtoH
-    pipeline) and writes the masked words and canonical secrets back to host
-    memory.  Not the headline metric; recorded in DESIGN.md."""
+def host_mode(a, A, torch, ctx, dist=None, rank=0, world=1):
+    """End-to-end host-memory rate: ODOs and secrets live in
+    (pageable or page-locked) host memory; each step streams them through the
+    GPU in --batch-words batches (3-slot HtoD/compute/DtoH pipeline) and
+    writes the masked words and canonical secrets back to host memory.  Under
+    torchrun every rank streams its own W-word shard from its own host memory
+    over its own PCIe link (weak scaling, C5 on 8 GPUs = 32 Mi words per
+    rank); the timed region is bracketed by barriers, the time is the max
+    over ranks and `value` counts every rank's words.  Not the headline
+    metric; recorded in DESIGN.md."""
     import numpy as np
     W, n = a.words, a.parties
+    coll = dist is not None and dist.is_initialized()
     gen = ctx
     if a.host_devices:  # one context over several devices: per-GPU shards from host memory
         ctx = A.Context(ctx.prime, ctx.r, ctx.r_inv, devices=[int(d) for d in a.host_devices.split(",")])
@@ -229,22 +234,36 @@ def host_mode(a, A, torch, ctx):
     for _ in range(a.warmup):
         ctx.mask_input(mask_odos, sec_h, out=masked_h)
         ctx.recombine_verify(share_odos, out=ys_h)
+    torch.cuda.synchronize()
+    if coll:
+        dist.barrier()
     t0 = time.perf_counter()
     ok = True
     for _ in range(a.steps):
         _, f1 = ctx.mask_input(mask_odos, sec_h, out=masked_h)
         _, f2 = ctx.recombine_verify(share_odos, out=ys_h)
         ok &= f1 == -1 and f2 == -1
+    torch.cuda.synchronize()
+    if coll:
+        dist.barrier()
     el = time.perf_counter() - t0
     ok &= bool(np.array_equal(ys_h, plain_h))  # outputs, not only the verdicts
-    hbytes = (kbytes("k_mask", n) + kbytes("k_rv", n)) * W
-    line = {"metric": "secret words/s host-memory share+recombine (PCIe-inclusive)",
-            "value": W * a.steps / el, "unit": "words/s", "n_gpus": ctx.device_count, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": el * 1e3 / a.steps, "higher_is_better": True,
-            "verified": ok, "pinned_inputs": a.pin, "batch_words": a.batch_words,
-            "host_bytes_per_step": hbytes, "host_GBps": hbytes * a.steps / el / 1e9,
-            "config": {"workload": "K_MASK + K_RV from host memory", "words": W, "parties": n}}
-    emit(line)
+    if coll:
+        t = torch.tensor([el, 0.0 if ok else 1.0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, ok = t[0].item(), t[1].item() == 0.0
+    hbytes = (kbytes("k_mask", n) + kbytes("k_rv", n)) * W  # per rank
+    gpus = ctx.device_count * world
+    if rank == 0:
+        line = {"metric": "secret words/s host-memory share+recombine (PCIe-inclusive)",
+                "value": W * world * a.steps / el, "unit": "words/s", "n_gpus": gpus,
+                "steps": a.steps, "warmup": a.warmup, "ms_per_step": el * 1e3 / a.steps,
+                "higher_is_better": True, "scaling": "weak", "verified": ok,
+                "pinned_inputs": a.pin, "batch_words": a.batch_words,
+                "host_bytes_per_step": hbytes * world, "host_GBps": hbytes * world * a.steps / el / 1e9,
+                "config": {"workload": "K_MASK + K_RV from host memory", "words_per_rank": W,
+                           "parties": n, "parallelism": "dp%d" % gpus}}
+        emit(line)
     if a.pin:
         for arr in (mask_h, share_h, sec_h, masked_h, ys_h):
             ctx.host_unregister(arr)
@@ -384,7 +403,10 @@ def main():
 
     ctx = A.Context(TEST_PRIME, TEST_R, TEST_RINV, device=local)
     if a.mode == "host":
-        return host_mode(a, A, torch, ctx)
+        host_mode(a, A, torch, ctx, dist, rank, world)
+        if distributed:
+            dist.destroy_process_group()
+        return
     if a.scatter:
         scatter_mode(a, A, torch, dist, ctx, rank, world)
         if distributed:

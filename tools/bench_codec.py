@@ -76,4 +76,16 @@ out["exchange_decode"] = {"ms": t_xd, "GBps": (34 * P2 + nchars) / (t_xd * 1e-3)
                           "Mpairs_per_s": P2 / (t_xd * 1e-3) / 1e6}
 out["exchange_cpu_python_json"] = {"pairs": sample, "encode_Mpairs_per_s": sample / (t1 - t0) / 1e6,
                                    "decode_Mpairs_per_s": sample / (t2 - t1) / 1e6}
+# CPU reference point for base64: CPython's binascii (C, one thread; Jackson's
+# MIME_NO_LINEFEEDS variant is the same alphabet and padding) on 96 MiB
+import base64  # noqa: E402
+b_h = raw[: 3 << 25].cpu().numpy().tobytes()
+t0 = time.perf_counter()
+e_h = base64.b64encode(b_h)
+t1 = time.perf_counter()
+base64.b64decode(e_h, validate=True)
+t2 = time.perf_counter()
+nb = len(b_h) + len(e_h)
+out["b64_cpu_python_binascii"] = {"bytes": len(b_h), "encode_GBps": nb / (t1 - t0) / 1e9,
+                                  "decode_GBps": nb / (t2 - t1) / 1e9, "threads": 1}
 print(json.dumps(out))

@@ -10,7 +10,7 @@
 using namespace amph;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
-__global__ void k_fill(uint4* mag, uint8_t* neg, size_t nvals) {
+__global__ void k_fill(uint4* mag, uint8_t* neg, size_t nvals, int full) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvals; i += (size_t)gridDim.x * blockDim.x) {
     uint64_t x = i * 0x9E3779B97F4A7C15ull + 12345, a = (x ^ (x >> 29)) * 0xBF58476D1CE4E5B9ull;
     uint64_t b = (a ^ (a >> 31)) * 0x94D049BB133111EBull;
@@ -18,12 +18,15 @@ __global__ void k_fill(uint4* mag, uint8_t* neg, size_t nvals) {
     const int sh = (int)(i % 7) * 17;
     mag[i] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> (33 + sh % 31)) >> (i % 7 == 3 ? 31 : 0));
     if (i % 11 == 5) mag[i] = make_uint4((uint32_t)(a % 1000), 0, 0, 0);
+    // full: |x - a| for x, a uniform below a 127-bit prime, as the party sends (38-39 digits)
+    if (full) mag[i] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32) >> 1);
     neg[i] = (uint8_t)((b >> 40) & 1);
   }
 }
 
 int main(int argc, char** argv) {
   const int R = argc > 1 ? atoi(argv[1]) : 20;
+  const int full = argc > 2 ? atoi(argv[2]) : 0;  // 1: full-length magnitudes (752 MB of text)
   const size_t npairs = (size_t)8 << 20, nvals = 2 * npairs;
   uint4 *mag, *mag2;
   uint8_t *neg, *neg2;
@@ -36,7 +39,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&len, 8)); CK(hipMalloc(&bad, 8));
   void *s1, *s2;
   CK(hipMalloc(&s1, xenc_scratch_bytes(npairs)));
-  hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, mag, neg, nvals);
+  hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, mag, neg, nvals, full);
   LaunchCfg c{0, 0, 256};
   CK(launch_exchange_encode(mag, neg, npairs, text, len, s1, c));
   unsigned long long L;
