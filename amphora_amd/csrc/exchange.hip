@@ -230,6 +230,40 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* total)
   return r;
 }
 
+// Inclusive wave scan of 32-bit values with DPP: row_shr 1/2/4/8 scans each
+// 16-lane row, row_bcast 15/31 carries the row totals (6 VALU with DPP
+// operands where a __shfl_up ladder costs ~40 VALU and six ds_bpermute).
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
+// Exclusive workgroup scan of 32-bit values (the decode's per-lane colon
+// counts: <= 32 per lane, <= 8192 per workgroup).
+__device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t* total) {
+  __shared__ uint32_t wsum32[17];
+  const int lane = __lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint32_t inc = wave_incl_scan32(v);
+  if (lane == 63) wsum32[wave] = inc;
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t s = lane < nw ? wsum32[lane] : 0;
+    const uint32_t si = wave_incl_scan32(s);
+    if (lane < nw) wsum32[lane] = si - s;  // exclusive wave offsets
+    if (lane == nw - 1) wsum32[16] = si;
+  }
+  __syncthreads();
+  const uint32_t r = wsum32[wave] + inc - v;
+  *total = wsum32[16];
+  __syncthreads();
+  return r;
+}
+
 __global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const uint64_t* x, size_t n,
                                                         uint64_t* bsum) {
   const size_t i = (size_t)blockIdx.x * kScanBlock + threadIdx.x;
@@ -396,12 +430,17 @@ __device__ __forceinline__ uint32_t swar_colon(uint32_t w) {
   const uint32_t x = w ^ 0x3A3A3A3Au;
   return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
 }
-__device__ __forceinline__ uint32_t colons32(const uint32_t (&w)[8]) {  // one bit per byte
+// One bit per byte: swar_colon leaves 0x80 in each ':' byte, and one
+// v_dot4_u32_u8 per dword with byte weights (1,2,4,8) or (16,32,64,128)
+// gathers two dwords' flags into bits 7..14 of their sum (12 VALU per 8 bytes
+// where shifting and OR-ing the flags together took ~20).
+__device__ __forceinline__ uint32_t colons32(const uint32_t (&w)[8]) {
   uint32_t m = 0;
 #pragma unroll
-  for (int d = 0; d < 8; ++d) {
-    const uint32_t c = swar_colon(w[d]) >> 7;
-    m |= ((c | (c >> 7) | (c >> 14) | (c >> 21)) & 0xFu) << (4 * d);
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t hi = __builtin_amdgcn_udot4(swar_colon(w[2 * q + 1]), 0x80402010u, 0u, false);
+    const uint32_t a = __builtin_amdgcn_udot4(swar_colon(w[2 * q]), 0x08040201u, hi, false);
+    m |= (a >> 7) << (8 * q);
   }
   return m;
 }
@@ -508,21 +547,43 @@ __device__ __forceinline__ void fold(uint32_t (&v)[4], uint32_t mul, uint32_t ad
   ovf |= carry != 0;
 }
 
-// 8 ASCII digits (little-endian bytes, first digit lowest) -> value < 10^8
-__device__ __forceinline__ uint32_t digits4(uint32_t w) {
-  const uint32_t v = w - 0x30303030u;
-  const uint32_t t = v * 10u + (v >> 8);
-  return (t & 0xFFu) * 100u + ((t >> 16) & 0xFFu);
-}
+// 8 ASCII digits (little-endian bytes, first digit lowest) -> value < 10^8:
+// v_dot4_u32_u8 forms the four 2-digit pairs straight from the ASCII bytes
+// (each offset by 11 * '0' = 528), three 24-bit multiply-adds join them and
+// one subtraction removes the offsets (8 VALU where the 16-bit-field SWAR
+// took ~15).
 __device__ __forceinline__ uint32_t digits8(uint32_t lo, uint32_t hi) {
-  return digits4(lo) * 10000u + digits4(hi);
+  const uint32_t a = __builtin_amdgcn_udot4(lo, 0x0000010Au, 0u, false);  // 10 d0 + d1 + 528
+  const uint32_t b = __builtin_amdgcn_udot4(lo, 0x010A0000u, 0u, false);  // 10 d2 + d3 + 528
+  const uint32_t c = __builtin_amdgcn_udot4(hi, 0x0000010Au, 0u, false);
+  const uint32_t d = __builtin_amdgcn_udot4(hi, 0x010A0000u, 0u, false);
+  const uint32_t ab = __umul24(a, 100u) + b, cd = __umul24(c, 100u) + d;  // <= 63327
+  return __umul24(ab, 10000u) + cd - 528u * 1010101u;
 }
-__device__ __forceinline__ uint32_t pow10_small(uint32_t k) {  // k <= 8
-  uint32_t p = 1;
+__device__ __forceinline__ uint32_t pow10_small(uint32_t k) {  // k <= 7
+  return __umul24(__umul24((k & 1u) ? 10u : 1u, (k & 2u) ? 100u : 1u), (k & 4u) ? 10000u : 1u);
+}
+
+// Length of the digit run at the start of the 44 bytes d[0..10] (44 if all
+// are digits): SWAR non-digit flags (0x80 per byte), packed one bit per byte
+// by v_dot4_u32_u8 as in colons32, and one 64-bit count of trailing zeros
+// (where a compare-and-select chain over the 11 dwords took twice the VALU).
+__device__ __forceinline__ uint32_t digit_run(const uint32_t (&d)[11]) {
+  uint64_t mask = 1ull << 44;
 #pragma unroll
-  for (uint32_t i = 0; i < 8; ++i)
-    if (i < k) p *= 10u;
-  return p;
+  for (int q = 0; q < 6; ++q) {
+    uint32_t nd2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = 2 * q + h;
+      const uint32_t x = (j < 11 ? d[j] : 0u) ^ 0x30303030u;  // digits -> 0..9
+      nd2[h] = (((x & 0x7F7F7F7Fu) + 0x76767676u) | x) & 0x80808080u;
+    }
+    const uint32_t a = __builtin_amdgcn_udot4(nd2[0], 0x08040201u,
+                                              __builtin_amdgcn_udot4(nd2[1], 0x80402010u, 0u, false), false);
+    mask |= (uint64_t)(a >> 7) << (8 * q);
+  }
+  return (uint32_t)__builtin_ctzll(mask);
 }
 
 // Fast path for the layout Jackson writes (no whitespace):
@@ -565,13 +626,7 @@ __device__ __forceinline__ bool fast_parse(const uint32_t* l32, uint32_t o, bool
   uint32_t d[11];
 #pragma unroll
   for (int j = 0; j < 11; ++j) d[j] = lds_dword(l32, ds + 4 * j);
-  uint32_t nd = 44;
-#pragma unroll
-  for (int j = 10; j >= 0; --j) {
-    const uint32_t x = d[j] ^ 0x30303030u;  // digits -> 0..9
-    const uint32_t nondig = (((x & 0x7F7F7F7Fu) + 0x76767676u) | x) & 0x80808080u;
-    if (nondig) nd = 4 * j + (__builtin_ctz(nondig) >> 3);
-  }
+  const uint32_t nd = digit_run(d);
   ok = ok && nd >= 1 && nd <= 39 && !((d[0] & 0xFFu) == (uint32_t)'0' && nd > 1);
   if (!ok) return false;
   r.dend = ds + nd;
@@ -624,13 +679,7 @@ __device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, boo
   uint32_t d[11];
 #pragma unroll
   for (int j = 0; j < 11; ++j) d[j] = lds_dword(l32, ds + 4 * j);
-  uint32_t nd = 44;
-#pragma unroll
-  for (int j = 10; j >= 0; --j) {
-    const uint32_t x = d[j] ^ 0x30303030u;  // digits -> 0..9
-    const uint32_t nondig = (((x & 0x7F7F7F7Fu) + 0x76767676u) | x) & 0x80808080u;
-    if (nondig) nd = 4 * j + (__builtin_ctz(nondig) >> 3);
-  }
+  const uint32_t nd = digit_run(d);
   ok = ok && nd >= 1 && nd <= 39 && !((d[0] & 0xFFu) == (uint32_t)'0' && nd > 1);
   if (!ok) return false;
   r.dend = ds + nd;
@@ -737,15 +786,15 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_slow(Text text, const uint64
   const uint4 c0 = win4[lo / 16], c1 = win4[lo / 16 + 1];
   const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
   uint32_t m = colons32(w);  // this lane's colons: one value each
-  uint64_t total;
-  const uint64_t first = block_excl_scan(__popc(m), &total);
+  uint32_t total;
+  const uint32_t first = block_excl_scan32(__popc(m), &total);
   for (int k = (int)first; m; m &= m - 1, ++k) {
     const int at = kDecBytes * threadIdx.x + __ffs(m) - 1;
     if (k < kMaxStarts) pos[k] = (uint16_t)at;
     else if (k == kMaxStarts) atomicMin(bad, (unsigned long long)(b0 + at - text.mis));
   }
   __syncthreads();
-  const uint32_t nloc = (uint32_t)min(total, (uint64_t)kMaxStarts);
+  const uint32_t nloc = min(total, (uint32_t)kMaxStarts);
   const uint64_t gbase = bscan[span] & kCountMask;
   // phase 1: own checks + value
   const uint32_t* l32 = reinterpret_cast<const uint32_t*>(win4);
@@ -896,13 +945,13 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64
   const uint4 c0 = win4[lo / 16], c1 = win4[lo / 16 + 1];
   const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
   uint32_t m = colons32(w);
-  uint64_t total;
-  const uint64_t first = block_excl_scan(__popc(m), &total);
+  uint32_t total;
+  const uint32_t first = block_excl_scan32(__popc(m), &total);
   for (int k = (int)first; m && k < kMaxStarts; m &= m - 1, ++k)
     pos[k] = (uint16_t)(kDecBytes * threadIdx.x + __ffs(m) - 1);
   __syncthreads();
-  bool fail = total > (uint64_t)kMaxStarts;
-  const uint32_t nloc = (uint32_t)min(total, (uint64_t)kMaxStarts);
+  bool fail = total > (uint32_t)kMaxStarts;
+  const uint32_t nloc = min(total, (uint32_t)kMaxStarts);
   const uint64_t gbase = bscan[blockIdx.x] & kCountMask;
   const uint32_t* l32 = reinterpret_cast<const uint32_t*>(win4);
   const size_t len = text.L - text.mis;
