@@ -338,7 +338,7 @@ __global__ __launch_bounds__(kXBlock) void k_xenc_write(const uint4* mag, const 
   uint32_t cd[5], ce[5];
   int nd = 0, ne = 0;
   bool sd = false, se = false;
-  uint64_t len = 0, total;
+  uint32_t len = 0, total;  // <= 92 per entry, <= 23 552 per workgroup
   if (k < npairs) {
     const uint4 d = mag[2 * k], e = mag[2 * k + 1];
     nd = to_chunks(d, cd);
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(kXBlock) void k_xenc_write(const uint4* mag, const 
     se = neg[2 * k + 1] != 0 && !is_zero(e);
     len = 11 + nd + sd + ne + se + (k + 1 < npairs);
   }
-  const uint64_t loc = block_excl_scan(len, &total);
+  const uint32_t loc = block_excl_scan32(len, &total);
   const uint64_t base = bs[blockIdx.x];
   char* dst = out + 1 + base;  // out[0] = '['
   const size_t sh = (uintptr_t)dst & 15;
@@ -939,7 +939,21 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64
   __shared__ uint16_t pos[kMaxStarts];  // colon, relative to b0
   const size_t b0 = (size_t)blockIdx.x * kDecSpan;
   const long long w0 = (long long)b0 - kWinPad;
-  for (int c = threadIdx.x; c < kWin / 16 + 1; c += kDecBlock) win4[c] = text.chunk(w0 + 16LL * c);
+  if (w0 >= (long long)text.mis && w0 + 16LL * (kWin / 16 + 1) <= (long long)text.L) {
+    // a window wholly inside the text: its 545 chunks as three plain 16-byte
+    // loads per lane, all issued before any is written (the third clamped:
+    // lanes past the window reload its last chunk and skip the write)
+    static_assert(kWin / 16 + 1 <= 3 * kDecBlock && kWin / 16 + 1 > 2 * kDecBlock, "three chunks per lane");
+    const u32x4* a = reinterpret_cast<const u32x4*>(text.al + w0);
+    const int c2 = min((int)threadIdx.x + 2 * kDecBlock, kWin / 16);
+    const u32x4 v0 = __builtin_nontemporal_load(a + threadIdx.x),
+                v1 = __builtin_nontemporal_load(a + threadIdx.x + kDecBlock), v2 = __builtin_nontemporal_load(a + c2);
+    win4[threadIdx.x] = make_uint4(v0.x, v0.y, v0.z, v0.w);
+    win4[threadIdx.x + kDecBlock] = make_uint4(v1.x, v1.y, v1.z, v1.w);
+    if ((int)threadIdx.x + 2 * kDecBlock <= kWin / 16) win4[c2] = make_uint4(v2.x, v2.y, v2.z, v2.w);
+  } else {
+    for (int c = threadIdx.x; c < kWin / 16 + 1; c += kDecBlock) win4[c] = text.chunk(w0 + 16LL * c);
+  }
   __syncthreads();
   const int lo = kWinPad + kDecBytes * threadIdx.x;
   const uint4 c0 = win4[lo / 16], c1 = win4[lo / 16 + 1];
