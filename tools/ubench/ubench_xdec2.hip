@@ -2,7 +2,10 @@
 // signed diffs encoded on the GPU (Jackson's compact layout), then the whole
 // product launch_exchange_decode (count, scan, parse, check) timed; every
 // decoded magnitude / sign compared with the encoder's input.
-#include "../../amphora_amd/csrc/exchange.hip"
+#ifndef XDEC_SRC
+#define XDEC_SRC "../../amphora_amd/csrc/exchange.hip"
+#endif
+#include XDEC_SRC
 #include <algorithm>
 #include <cstdio>
 #include <vector>
