@@ -123,6 +123,7 @@ struct amph_ctx {
   DevBuf ff;  // per-batch first-fail words (host path)
   DevBuf tail;  // small scratch for the partial last unit of codec calls
   DevBuf wire;  // host-mode staging of the wire-text calls (texts, secrets, outputs, verdicts)
+  DevBuf xstage;  // host-mode staging of the exchange codec calls
   std::unique_ptr<amph::CopyPool> pool;
 };
 
@@ -623,6 +624,7 @@ void amph_ctx_destroy(amph_ctx* c) {
     c->ff.release();
     c->tail.release();
     c->wire.release();
+    c->xstage.release();
   }
   delete c;
 }
@@ -1185,6 +1187,29 @@ int host_stream0(amph_ctx* c, hipStream_t* s) {
   *s = c->streams[0];
   return AMPH_OK;
 }
+
+// Host-mode buffers of the exchange codec calls: carved from one per-context
+// device arena (grown with hipMalloc, held under the context mutex).  Two
+// contexts on one device calling at the same time once got overlapping
+// stream-ordered (hipMallocAsync) staging buffers: each party's exchange
+// text came back empty or overwritten (tools/c1_native, two party threads).
+struct XStage {
+  uint8_t* base = nullptr;
+  size_t off = 0;
+  int stage(amph_ctx* c, const size_t* sizes, int n) {
+    size_t total = 0;
+    for (int i = 0; i < n; ++i) total += align256(sizes[i] ? sizes[i] : 16);
+    hipError_t e = c->xstage.ensure(total);
+    if (e != hipSuccess) return fail(AMPH_E_NOMEM, "exchange staging");
+    base = (uint8_t*)c->xstage.p;
+    return AMPH_OK;
+  }
+  void* take(size_t bytes) {
+    void* p = base + off;
+    off += align256(bytes ? bytes : 16);
+    return p;
+  }
+};
 }  // namespace
 
 int amph_exchange_encode(amph_ctx* c, const uint8_t* mag16, const uint8_t* neg, size_t npairs,
@@ -1207,27 +1232,25 @@ int amph_exchange_encode(amph_ctx* c, const uint8_t* mag16, const uint8_t* neg, 
   std::lock_guard<std::mutex> g(c->mu);
   hipStream_t s;
   if (int st = host_stream0(c, &s)) return st;
-  AsyncBuf dmag, dneg, dout, dlen, scratch;
-  HIP_TRY(dmag.alloc(32 * npairs, s));
-  HIP_TRY(dneg.alloc(2 * npairs, s));
-  HIP_TRY(dout.alloc(maxb, s));
-  HIP_TRY(dlen.alloc(8, s));
-  HIP_TRY(scratch.alloc(amph::xenc_scratch_bytes(npairs), s));
-  HIP_TRY(hipStreamSynchronize(s));  // the stream-ordered allocations exist; blocking copies in
+  XStage x;
+  const size_t sizes[5] = {32 * npairs, 2 * npairs, maxb, 8, amph::xenc_scratch_bytes(npairs)};
+  if (int st = x.stage(c, sizes, 5)) return st;
+  void *dmag = x.take(sizes[0]), *dneg = x.take(sizes[1]), *dout = x.take(sizes[2]), *dlen = x.take(sizes[3]),
+       *scratch = x.take(sizes[4]);
   if (npairs) {
-    HIP_TRY(hipMemcpy(dmag.p, mag16, 32 * npairs, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(dneg.p, neg, 2 * npairs, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dmag, mag16, 32 * npairs, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dneg, neg, 2 * npairs, hipMemcpyHostToDevice));
   }
-  hipError_t e = amph::launch_exchange_encode((const uint4*)dmag.p, (const uint8_t*)dneg.p, npairs,
-                                              (char*)dout.p, (unsigned long long*)dlen.p, scratch.p,
+  hipError_t e = amph::launch_exchange_encode((const uint4*)dmag, (const uint8_t*)dneg, npairs,
+                                              (char*)dout, (unsigned long long*)dlen, scratch,
                                               cfg(c, s, npairs));
   if (e != hipSuccess) return hip_fail(e, "k_xenc");
   uint64_t len = 0;
-  HIP_TRY(read_back(s, {{&len, dlen.p, 8}}));
+  HIP_TRY(read_back(s, {{&len, dlen, 8}}));
   *out_len = len;
   if (len > out_cap) return fail(AMPH_E_LEN, "output capacity " + std::to_string(out_cap) +
                                                  " below the encoded length " + std::to_string(len));
-  HIP_TRY(read_back(s, {{out, dout.p, len}}));
+  HIP_TRY(read_back(s, {{out, dout, len}}));
   return AMPH_OK;
 }
 
@@ -1249,21 +1272,19 @@ int amph_exchange_decode(amph_ctx* c, const char* text, size_t len, size_t npair
   std::lock_guard<std::mutex> g(c->mu);
   hipStream_t s;
   if (int st = host_stream0(c, &s)) return st;
-  AsyncBuf dtext, dmag, dneg, dbad, scratch;
-  HIP_TRY(dtext.alloc(len, s));
-  HIP_TRY(dmag.alloc(32 * npairs, s));
-  HIP_TRY(dneg.alloc(2 * npairs, s));
-  HIP_TRY(dbad.alloc(8, s));
-  HIP_TRY(scratch.alloc(amph::xdec_scratch_bytes(len), s));
-  HIP_TRY(hipStreamSynchronize(s));  // the stream-ordered allocations exist; blocking copy in
-  if (len) HIP_TRY(hipMemcpy(dtext.p, text, len, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemsetAsync(dbad.p, 0x7F, 8, s));
-  hipError_t e = amph::launch_exchange_decode((const char*)dtext.p, len, npairs, (uint4*)dmag.p,
-                                              (uint8_t*)dneg.p, (unsigned long long*)dbad.p, scratch.p,
+  XStage x;
+  const size_t sizes[5] = {len, 32 * npairs, 2 * npairs, 8, amph::xdec_scratch_bytes(len)};
+  if (int st = x.stage(c, sizes, 5)) return st;
+  void *dtext = x.take(sizes[0]), *dmag = x.take(sizes[1]), *dneg = x.take(sizes[2]), *dbad = x.take(sizes[3]),
+       *scratch = x.take(sizes[4]);
+  if (len) HIP_TRY(hipMemcpy(dtext, text, len, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemsetAsync(dbad, 0x7F, 8, s));
+  hipError_t e = amph::launch_exchange_decode((const char*)dtext, len, npairs, (uint4*)dmag,
+                                              (uint8_t*)dneg, (unsigned long long*)dbad, scratch,
                                               cfg(c, s, len));
   if (e != hipSuccess) return hip_fail(e, "k_xdec");
   int64_t bad = 0;
-  HIP_TRY(read_back(s, {{&bad, dbad.p, 8}}));
+  HIP_TRY(read_back(s, {{&bad, dbad, 8}}));
   const bool ok = bad == (int64_t)AMPH_NO_FAILURE;
   if (bad_index) *bad_index = ok ? -1 : bad;
   if (!ok) {
@@ -1271,7 +1292,7 @@ int amph_exchange_decode(amph_ctx* c, const char* text, size_t len, size_t npair
       return fail(AMPH_E_LEN, "interimValues must hold exactly " + std::to_string(npairs) + " FactorPairs");
     return fail(AMPH_E_PARAM, "Malformed FactorPair JSON at offset " + std::to_string(bad));
   }
-  HIP_TRY(read_back(s, {{mag16, dmag.p, 32 * npairs}, {neg, dneg.p, 2 * npairs}}));
+  HIP_TRY(read_back(s, {{mag16, dmag, 32 * npairs}, {neg, dneg, 2 * npairs}}));
   return AMPH_OK;
 }
 

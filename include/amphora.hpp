@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <exception>
 #include <functional>
 #include <stdexcept>
 #include <string>
@@ -546,8 +547,8 @@ class OutputDeliveryService {
         if (pd.first != op) throw IllegalArgumentException("operation id mismatch");
         partners.push_back(std::move(pd.second));
       }
-    } catch (const std::exception&) {
-      throw AmphoraServiceException("Failed to open values for operation #" + op);
+    } catch (const std::exception&) {  // the cause stays attached (std::rethrow_if_nested), as Java chains it
+      std::throw_with_nested(AmphoraServiceException("Failed to open values for operation #" + op));
     }
     std::vector<const uint8_t*> mags{own.mag.data()}, negs{own.neg.data()};
     for (auto& pd : partners) {
@@ -568,7 +569,7 @@ class OutputDeliveryService {
     try {
       b = tuples_(id, type, count);
     } catch (const std::exception&) {  // :103-107, :178-185
-      throw AmphoraServiceException("Failed to retrieve the required Tuples form Castor");
+      std::throw_with_nested(AmphoraServiceException("Failed to retrieve the required Tuples form Castor"));
     }
     if (b.size() != count * width)
       throw AmphoraServiceException("Failed to retrieve the required Tuples form Castor");

@@ -24,3 +24,17 @@ def test_cpp_mirror_cpu():
 def test_cpp_mirror_gpu():
     r = subprocess.run([_bin(), "gpu"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_c1_native_round_trip():
+    """BASELINE config C1 through the C++ mirror: upload + download of a
+    ragged word count over two in-process parties (JSON open between party
+    threads), secrets back bit-exact (tools/c1_native.cpp)."""
+    import build_native
+    import json
+    r = subprocess.run([build_native.build_c1_native(), "1001", "2"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["bit_exact_round_trip"] is True and line["words"] == 1001

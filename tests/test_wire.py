@@ -264,6 +264,42 @@ def test_exchange_encode_matches_jackson(ctx, n):
     assert np.array_equal(n2, neg_exp)
 
 
+def test_exchange_host_calls_from_two_contexts_at_once(ctx):
+    """Two parties' contexts on one GPU coding their opens at the same time
+    (the loopback's party threads; ctypes drops the GIL): every text and
+    every decode stays exact.  With stream-ordered (hipMallocAsync) staging
+    the two calls once received overlapping buffers (empty / overwritten
+    texts in tools/c1_native)."""
+    import threading
+    import amphora_amd as A
+    from amphora_amd import wire
+    ctxs = [ctx, A.Context(P, R, RINV)]
+    jobs = []
+    for j in range(2):
+        pairs = _random_pairs(8192 + 37 * j, 50 + j)
+        mag, neg = _diff_arrays(pairs)
+        jobs.append((mag, neg, _jackson(uuid.UUID(int=j), j, pairs)))
+    errors = []
+
+    def party(j):
+        mag, neg, expect = jobs[j]
+        try:
+            for _ in range(30):
+                body = wire.exchange_to_json(ctxs[j], uuid.UUID(int=j), j, mag, neg)
+                assert body == expect
+                _, _, m2, _ = wire.exchange_from_json(ctxs[j], body, mag.shape[0])
+                assert np.array_equal(m2, mag)
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((j, repr(e)[:300]))
+
+    th = [threading.Thread(target=party, args=(j,)) for j in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+
+
 def test_exchange_device_mode(ctx):
     import torch
     from amphora_amd import wire

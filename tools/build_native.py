@@ -70,6 +70,25 @@ def build_cpp_test(force: bool = False) -> str:
     return CPP_TEST_BIN
 
 
+C1_SRC = os.path.join(ROOT, "tools", "c1_native.cpp")
+C1_BIN = os.path.join(ROOT, "tools", "c1_native")
+
+
+def build_c1_native(force: bool = False) -> str:
+    """BASELINE config C1 through the C++ mirror (tools/c1_native.cpp)."""
+    deps = [C1_SRC, os.path.join(ROOT, "include", "amphora.hpp"), LIB]
+    if not force and os.path.exists(C1_BIN) and all(
+            os.path.getmtime(d) <= os.path.getmtime(C1_BIN) for d in deps):
+        return C1_BIN
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-pthread", "-I" + os.path.join(ROOT, "include"), C1_SRC,
+           "-L" + HERE, "-lamphora_hip", "-Wl,-rpath,$ORIGIN/../amphora_amd", "-o", C1_BIN]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("g++ failed building tools/c1_native")
+    return C1_BIN
+
+
 SAN_DIR = os.path.join(ROOT, "build", "sanitize")
 SAN_FLAGS = ["-fsanitize=address", "-fsanitize=undefined", "-fno-sanitize-recover=all",
              "-fno-omit-frame-pointer"]
