@@ -124,6 +124,8 @@ struct amph_ctx {
   DevBuf tail;  // small scratch for the partial last unit of codec calls
   DevBuf wire;  // host-mode staging of the wire-text calls (texts, secrets, outputs, verdicts)
   DevBuf xstage;  // host-mode staging of the exchange codec calls
+  DevBuf xdev;    // device-mode scan scratch of the exchange codec calls
+  hipEvent_t xdev_done = nullptr;  // the last device-mode exchange call's kernels
   std::unique_ptr<amph::CopyPool> pool;
 };
 
@@ -626,6 +628,12 @@ void amph_ctx_destroy(amph_ctx* c) {
     c->wire.release();
     c->xstage.release();
   }
+  if (c->xdev_done) {
+    (void)hipSetDevice(c->device);
+    (void)hipEventSynchronize(c->xdev_done);
+    (void)hipEventDestroy(c->xdev_done);
+  }
+  c->xdev.release();
   delete c;
 }
 
@@ -1170,17 +1178,22 @@ size_t amph_exchange_max_chars(size_t npairs) { return amph::xenc_max_bytes(npai
 namespace {
 // Host-pointer calls of the exchange codec: one shot on the context's first
 // stream (the whole text is scanned at once, so there is no batching).
-struct AsyncBuf {
-  void* p = nullptr;
-  hipStream_t s = nullptr;
-  hipError_t alloc(size_t bytes, hipStream_t st) {
-    s = st;
-    return hipMallocAsync(&p, bytes ? bytes : 16, st);
+//
+// Device-pointer calls take their scan scratch from one per-context buffer:
+// under the context mutex each call makes its stream wait for the previous
+// call's kernels (xdev_done) before reusing it, then records its own.  (The
+// device's stream-ordered pool handed two contexts overlapping buffers in
+// the host paths)
+int dev_scratch(amph_ctx* c, size_t bytes, hipStream_t s, void** p) {
+  if (!c->xdev_done) HIP_TRY(hipEventCreateWithFlags(&c->xdev_done, hipEventDisableTiming));
+  else HIP_TRY(hipStreamWaitEvent(s, c->xdev_done, 0));
+  if (c->xdev.cap < bytes) {
+    HIP_TRY(hipEventSynchronize(c->xdev_done));  // the old buffer is idle before it is freed
+    if (c->xdev.ensure(bytes) != hipSuccess) return fail(AMPH_E_NOMEM, "exchange scratch");
   }
-  ~AsyncBuf() {
-    if (p) (void)hipFreeAsync(p, s);
-  }
-};
+  *p = c->xdev.p;
+  return AMPH_OK;
+}
 
 int host_stream0(amph_ctx* c, hipStream_t* s) {
   if (!c->streams[0]) HIP_TRY(hipStreamCreateWithFlags(&c->streams[0], hipStreamNonBlocking));
@@ -1223,11 +1236,14 @@ int amph_exchange_encode(amph_ctx* c, const uint8_t* mag16, const uint8_t* neg, 
     if (int st = check_dev_words({mag16})) return st;
     if (out_cap < maxb) return fail(AMPH_E_LEN, "output capacity below amph_exchange_max_chars(npairs)");
     hipStream_t s = (hipStream_t)stream;
-    AsyncBuf scratch;
-    HIP_TRY(scratch.alloc(amph::xenc_scratch_bytes(npairs), s));
+    std::lock_guard<std::mutex> g(c->mu);
+    void* scratch;
+    if (int st = dev_scratch(c, amph::xenc_scratch_bytes(npairs), s, &scratch)) return st;
     hipError_t e = amph::launch_exchange_encode((const uint4*)mag16, neg, npairs, out,
-                                                (unsigned long long*)out_len, scratch.p, cfg(c, s, npairs));
-    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_xenc");
+                                                (unsigned long long*)out_len, scratch, cfg(c, s, npairs));
+    if (e != hipSuccess) return hip_fail(e, "k_xenc");
+    HIP_TRY(hipEventRecord(c->xdev_done, s));
+    return AMPH_OK;
   }
   std::lock_guard<std::mutex> g(c->mu);
   hipStream_t s;
@@ -1263,11 +1279,14 @@ int amph_exchange_decode(amph_ctx* c, const char* text, size_t len, size_t npair
     if (int st = check_dev_words({mag16})) return st;
     hipStream_t s = (hipStream_t)stream;
     if (int st = reset_ff_dev(bad_index, flags, s)) return st;
-    AsyncBuf scratch;
-    HIP_TRY(scratch.alloc(amph::xdec_scratch_bytes(len), s));
+    std::lock_guard<std::mutex> g(c->mu);
+    void* scratch;
+    if (int st = dev_scratch(c, amph::xdec_scratch_bytes(len), s, &scratch)) return st;
     hipError_t e = amph::launch_exchange_decode(text, len, npairs, (uint4*)mag16, neg,
-                                                (unsigned long long*)bad_index, scratch.p, cfg(c, s, len));
-    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_xdec");
+                                                (unsigned long long*)bad_index, scratch, cfg(c, s, len));
+    if (e != hipSuccess) return hip_fail(e, "k_xdec");
+    HIP_TRY(hipEventRecord(c->xdev_done, s));
+    return AMPH_OK;
   }
   std::lock_guard<std::mutex> g(c->mu);
   hipStream_t s;
