@@ -38,3 +38,16 @@ def test_c1_native_round_trip():
     assert r.returncode == 0, r.stdout + r.stderr
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["bit_exact_round_trip"] is True and line["words"] == 1001
+
+
+@pytest.mark.gpu
+def test_c1_native_three_parties_shared_context():
+    """The same flow with three parties (two partner texts per open) whose
+    threads all call into one context at once."""
+    import build_native
+    import json
+    r = subprocess.run([build_native.build_c1_native(), "777", "2", "shared", "3"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["bit_exact_round_trip"] is True and line["parties"] == 3 and line["contexts"] == 1

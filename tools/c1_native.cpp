@@ -17,7 +17,7 @@
 //
 // Every word of share arithmetic runs on the GPU; the host code is what a
 // JNI-bound Java host would run around it.  Usage:
-//   c1_native [words=1024] [reps=20] [shared]   -> one JSON line on stdout
+//   c1_native [words=1024] [reps=20] [shared|own] [parties=2]   -> one JSON line on stdout
 // ("shared": both parties on one context, called from both threads at once)
 #include <algorithm>
 #include <chrono>
@@ -313,19 +313,21 @@ int main(int argc, char** argv) {
   const size_t W = argc > 1 ? std::stoul(argv[1]) : 1024;
   const int reps = argc > 2 ? std::stoi(argv[2]) : 20;
   const bool shared = argc > 3 && std::string(argv[3]) == "shared";
+  const int n = argc > 4 ? std::stoi(argv[4]) : 2;  // parties
   const int warm = 3;
   try {
     std::mt19937_64 rng(1);
-    const std::vector<u128> macKeys = {(((u128)rng() << 64) | rng()) % P, (((u128)rng() << 64) | rng()) % P};
-    Dealer dealer(2, macKeys, 7);
-    Hub hub(2);
+    std::vector<u128> macKeys;
+    for (int j = 0; j < n; ++j) macKeys.push_back((((u128)rng() << 64) | rng()) % P);
+    Dealer dealer(n, macKeys, 7);
+    Hub hub(n);
     // one context per party (separate services), or "shared": both parties'
     // threads call into one context at the same time (one service's request
     // threads sharing its SecretShareUtil bean)
     std::vector<std::unique_ptr<Context>> ctxs;
-    for (int j = 0; j < (shared ? 1 : 2); ++j) ctxs.emplace_back(new Context(P, R, RI));
+    for (int j = 0; j < (shared ? 1 : n); ++j) ctxs.emplace_back(new Context(P, R, RI));
     std::vector<std::unique_ptr<Party>> parties;
-    for (int j = 0; j < 2; ++j) parties.emplace_back(new Party(j, macKeys[j], *ctxs[shared ? 0 : j], dealer, hub));
+    for (int j = 0; j < n; ++j) parties.emplace_back(new Party(j, macKeys[j], *ctxs[shared ? 0 : j], dealer, hub));
     auto util = client::SecretShareUtil::of(P, R, RI);
     // the dealer's Montgomery encoding against the library's toGfp
     {
@@ -375,11 +377,11 @@ int main(int argc, char** argv) {
         down.push_back(td);
       }
     }
-    std::printf("{\"tool\": \"c1_native\", \"words\": %zu, \"parties\": 2, \"contexts\": %d, \"reps\": %d, "
+    std::printf("{\"tool\": \"c1_native\", \"words\": %zu, \"parties\": %d, \"contexts\": %d, \"reps\": %d, "
                 "\"upload_ms_median\": %.3f, \"upload_ms_min\": %.3f, \"download_ms_median\": %.3f, "
                 "\"download_ms_min\": %.3f, \"bit_exact_round_trip\": %s, \"host\": \"C++ mirror "
                 "(include/amphora.hpp), one thread per party per call, JSON open between parties\"}\n",
-                W, shared ? 1 : 2, reps, median(up), *std::min_element(up.begin(), up.end()), median(down),
+                W, n, shared ? 1 : n, reps, median(up), *std::min_element(up.begin(), up.end()), median(down),
                 *std::min_element(down.begin(), down.end()), exact ? "true" : "false");
     return exact ? 0 : 1;
   } catch (const std::exception& e) {
