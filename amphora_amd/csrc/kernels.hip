@@ -38,6 +38,25 @@ __device__ __forceinline__ uint4 ld(const uint4* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void st(uint4* p, const W4& v) { *p = u4(v); }
+// Result words (K_RV / K_MASK and their wire forms, the open, the products):
+// nontemporal 16-byte stores.  Measured in bench.py on one box, alternating
+// builds 3x: C2 14.6-15.0 -> 15.6-15.8 G words/s, C3 10.7-10.8 -> 11.0-11.2;
+// k_open / k_open_post -7 % at 16 Mi words (profiles/r02_ab_store_policy.txt).
+// Plain stores left each kernel's output dirty in the caches for the next
+// launch to drain.  (Round 1's ubench_store had preferred plain stores at
+// 16 Mi words.)  Intermediates read again at once (K_ODO_PRE's diffs) keep
+// plain stores.
+#ifndef AMPH_ST_NT
+#define AMPH_ST_NT 1
+#endif
+__device__ __forceinline__ void st_out(uint4* p, const W4& v) {
+  if constexpr (AMPH_ST_NT) {
+    const uint4 x = u4(v);
+    __builtin_nontemporal_store(u32x4{x.x, x.y, x.z, x.w}, reinterpret_cast<u32x4*>(p));
+  } else {
+    *p = u4(v);
+  }
+}
 
 // Wave-level reduction of the failing indices to one atomic per wave: the
 // lowest set lane holds the smallest index of this iteration.
@@ -100,7 +119,7 @@ __global__ __launch_bounds__(kMaxBlock) void k_rv(OdoSet odo, int n, size_t word
     W4 a[5];
     recombine5<NP, BIG>(odo, n, i, f, a);
     const bool ok = (int)eq(mont_mul(a[0], a[1], f), a[3]) & (int)eq(mont_mul(a[2], a[1], f), a[4]);
-    if constexpr (WRITE_Y) st(out_y + i, redc(a[0], f));
+    if constexpr (WRITE_Y) st_out(out_y + i, redc(a[0], f));
     report_fail(!ok, ibase + i, ff);
   }
 }
@@ -125,7 +144,7 @@ __global__ __launch_bounds__(kMaxBlock) void k_mask(OdoSet odo, int n, size_t wo
     const bool ok = (int)eq(mont_mul(a[0], a[1], f), a[3]) & (int)eq(mont_mul(a[2], a[1], f), a[4]);
     // the secret's product in the product-scanning form: 64 instead of 65
     // VGPRs at 3 parties (8 waves per SIMD: two 1024-lane workgroups per CU)
-    st(out + i, mod_sub(MASK_SECRET_MUL(w4(s), r2, f), a[0], f));
+    st_out(out + i, mod_sub(MASK_SECRET_MUL(w4(s), r2, f), a[0], f));
     report_fail(!ok, i, ff);
   }
 }
@@ -135,7 +154,7 @@ __global__ __launch_bounds__(kMaxBlock) void k_recombine(ShareSet sh, int n, siz
                                                      uint4* out, Fp f) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride)
-    st(out + i, redc(sum_field<NP, BIG>(sh.s, n, i, f), f));
+    st_out(out + i, redc(sum_field<NP, BIG>(sh.s, n, i, f), f));
 }
 
 template <bool BIG>
@@ -276,7 +295,7 @@ __global__ __launch_bounds__(kMaxBlock) void k_open(SignedSet d, int n, size_t n
         acc = reinterpret_cast<const uint8_t*>(d.neg[j])[t] ? mod_sub(acc, x, f) : mod_add(acc, x, f);
       }
     }
-    st(out + t, acc);
+    st_out(out + t, acc);
   }
 }
 
@@ -311,7 +330,7 @@ __global__ __launch_bounds__(kPairBlock) void k_odo_post(const uint4* opened,
   const W4 D = canon<BIG>(w4(Dr), f), E = canon<BIG>(w4(Er), f);
   const W4 bb = p0 ? mod_add(canon<BIG>(b, f), mont_mul(E, r2, f), f) : b;
   const W4 x = dot2_redc(D, bb, E, a, f);  // D b + E a (+ D E), canonical
-  st((k & 1 ? ou : ow) + (k >> 1), mod_add(canon<BIG>(c, f), mont_mul(x, r2, f), f));
+  st_out((k & 1 ? ou : ow) + (k >> 1), mod_add(canon<BIG>(c, f), mont_mul(x, r2, f), f));
 }
 
 // recombineDiffs fused into K_ODO_POST (OutputDeliveryService.java:223-228,
@@ -378,7 +397,7 @@ __global__ __launch_bounds__(kPairBlock) void k_open_post(SignedSet d, int n, co
   const W4 r2 = r2_word(f);
   const W4 bb = p0 ? mod_add(canon<BIG>(b, f), mont_mul(E, r2, f), f) : b;
   const W4 x = dot2_redc(D, bb, E, a, f);
-  st((k & 1 ? ou : ow) + (k >> 1), mod_add(canon<BIG>(c, f), mont_mul(x, r2, f), f));
+  st_out((k & 1 ? ou : ow) + (k >> 1), mod_add(canon<BIG>(c, f), mont_mul(x, r2, f), f));
 }
 
 // MpSpdzIntegrationUtils.toGfp / fromGfp over arrays, and maskInput with
@@ -630,7 +649,7 @@ __global__ __launch_bounds__(BS) void k_rv_b64(TextSet tx, int n, size_t words, 
     bool ok = true;
     if (in) {
       ok = (int)eq(mont_mul_v(acc[0], acc[1], f), acc[3]) & (int)eq(mont_mul_v(acc[2], acc[1], f), acc[4]);
-      st(out_y + word, redc(acc[0], f));
+      st_out(out_y + word, redc(acc[0], f));
     }
     report_fail(in && !ok, word, ff);
   }
@@ -669,7 +688,7 @@ __global__ __launch_bounds__(BS) void k_mask_b64(TextSet tx, int n, size_t words
     report_fail(in && !ok, word, ff);
     if (has_secret) {
       const uint4 m = u4(mod_sub(mont_mul_v(w4(s), r2_word(f), f), acc[0], f));
-      if (out16) st(out16 + word, w4(m));
+      if (out16) st_out(out16 + word, w4(m));
       enc_word24(m, g);
     }
   }
@@ -717,7 +736,7 @@ __global__ __launch_bounds__(kMaxBlock) void k_stream_probe(OdoSet odo, int n, s
         x.z ^= v.z;
         x.w ^= v.w;
       }
-    out[i] = x;
+    st_out(out + i, w4(x));
   }
 }
 

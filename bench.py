@@ -77,7 +77,7 @@ def parse():
     ap.add_argument("--words", type=int, default=1 << 20, help="words per GPU (C2: 2^20)")
     ap.add_argument("--parties", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--samples", type=int, default=8,
+    ap.add_argument("--samples", type=int, default=32,
                     help="event-stamped launches per kernel, spread evenly over the timed "
                          "steps, at most one per step (each costs ~3-4 us of dispatch, "
                          "tools/step_overhead.py)")
