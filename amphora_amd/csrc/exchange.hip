@@ -39,6 +39,16 @@ namespace {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// Encoded text and fast-path decoded magnitudes leave through nontemporal
+// stores (AMPH_CODEC_NT=0 for A/B).
+#ifndef AMPH_CODEC_NT
+#define AMPH_CODEC_NT 1
+#endif
+__device__ __forceinline__ void xst16(uint4* p, uint4 v) {
+  if constexpr (AMPH_CODEC_NT) __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(p));
+  else *p = v;
+}
+
 constexpr int kXBlock = 256;      // pairs per workgroup (encode)
 constexpr int kXEntry = 92;       // max entry: {"a":-<39 digits>,"b":-<39 digits>},
 constexpr int kScanBlock = 1024;  // elements per workgroup of the scan passes
@@ -371,7 +381,7 @@ __global__ __launch_bounds__(kXBlock) void k_xenc_write(const uint4* mag, const 
   } else {
     if (sh + threadIdx.x < 16 * ulo) dal[sh + threadIdx.x] = buf[sh + threadIdx.x];
     for (size_t u = ulo + threadIdx.x; u < uhi; u += kXBlock)
-      reinterpret_cast<uint4*>(dal)[u] = bufv[u];
+      xst16(reinterpret_cast<uint4*>(dal) + u, bufv[u]);
     if (16 * uhi + threadIdx.x < endb) dal[16 * uhi + threadIdx.x] = buf[16 * uhi + threadIdx.x];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -975,7 +985,7 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64
     FastNum fn;
     if (g < nvals && fast_segment(l32, at + 1 + kWinPad, g, nvals, b0 + at + 1 - text.mis, len, fn)) {
       const size_t slot = (g & ~(uint64_t)1) + (fn.key == 'b');
-      mag[slot] = make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]);
+      xst16(mag + slot, make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]));
       neg[slot] = fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0;
     } else {
       fail = true;
