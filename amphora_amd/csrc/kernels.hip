@@ -58,6 +58,20 @@ __device__ __forceinline__ void st_out(uint4* p, const W4& v) {
   }
 }
 
+// Party-side outputs that the next stage reads at once (K_CONV's share
+// words, K_ODO_PRE's raw copies and diffs): nontemporal as well.  Alternated
+// A/B, 3x on one box: K_CONV and K_ODO_PRE -4 % at 16 Mi words, the exchange
+// encode that reads the diffs -8 %, party Output Delivery 4 Mi x 3
+// 1.81 -> 1.79 ms (profiles/r02_ab_store_policy.txt).  AMPH_PARTY_NT=0 for
+// plain stores.
+#ifndef AMPH_PARTY_NT
+#define AMPH_PARTY_NT 1
+#endif
+__device__ __forceinline__ void st_party(uint4* p, const uint4& x) {
+  if constexpr (AMPH_PARTY_NT) __builtin_nontemporal_store(u32x4{x.x, x.y, x.z, x.w}, reinterpret_cast<u32x4*>(p));
+  else *p = x;
+}
+
 // Wave-level reduction of the failing indices to one atomic per wave: the
 // lowest set lane holds the smallest index of this iteration.
 __device__ __forceinline__ void report_fail(bool bad, size_t i, unsigned long long* ff) {
@@ -223,7 +237,7 @@ __global__ __launch_bounds__(kPairBlock) void k_conv(const uint4* masked, const 
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const size_t q = (size_t)r * kPairBlock + threadIdx.x;
-    if (q < 2 * nblk) out[2 * i0 + q] = buf[(q >> 1) * 3 + (q & 1)];
+    if (q < 2 * nblk) st_party(out + 2 * i0 + q, buf[(q >> 1) * 3 + (q & 1)]);
   }
 }
 
@@ -254,16 +268,16 @@ __global__ __launch_bounds__(kPairBlock) void k_odo_pre(const uint4* share_data,
   const uint4 m1 = msk[lpair0 * 3], m2 = msk[(lpair0 + 1) * 3];
   const uint4 x = even ? yr : m2;
   if (even) {
-    oy[i] = yr;
-    orr[i] = m1;
+    st_party(oy + i, yr);
+    st_party(orr + i, m1);
   } else {
-    ov[i] = m2;
+    st_party(ov + i, m2);
   }
   W4 d, e;
   const uint32_t sd = signed_diff(redc(w4(x), f), redc(w4(a), f), d);
   const uint32_t se = signed_diff(redc(w4(m1), f), redc(w4(b), f), e);
-  st(omag + 2 * k, d);
-  st(omag + 2 * k + 1, e);
+  st_party(omag + 2 * k, u4(d));
+  st_party(omag + 2 * k + 1, u4(e));
   oneg[k] = (uint16_t)(sd | (se << 8));
 }
 
