@@ -33,9 +33,18 @@ namespace {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Streamed-once inputs: nontemporal 16-byte loads (global_load_dwordx4 nt).
+// Streamed-once inputs: nontemporal loads (AMPH_LD_NT=0 for A/B: plain loads
+// measured 8-10 % slower at C2 with the nontemporal stores in place).
+#ifndef AMPH_LD_NT
+#define AMPH_LD_NT 1
+#endif
 __device__ __forceinline__ uint4 ld(const uint4* p) {
-  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-  return make_uint4(v.x, v.y, v.z, v.w);
+  if constexpr (AMPH_LD_NT) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *p;
+  }
 }
 __device__ __forceinline__ void st(uint4* p, const W4& v) { *p = u4(v); }
 // Result words (K_RV / K_MASK and their wire forms, the open, the products):
