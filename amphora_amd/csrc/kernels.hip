@@ -32,9 +32,9 @@ namespace {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// Streamed-once inputs: nontemporal 16-byte loads (global_load_dwordx4 nt).
-// Streamed-once inputs: nontemporal loads (AMPH_LD_NT=0 for A/B: plain loads
-// measured 8-10 % slower at C2 with the nontemporal stores in place).
+// Streamed-once inputs: nontemporal 16-byte loads (global_load_dwordx4 nt;
+// AMPH_LD_NT=0 for A/B: plain loads measured 8-10 % slower at C2 with the
+// nontemporal stores in place).
 #ifndef AMPH_LD_NT
 #define AMPH_LD_NT 1
 #endif
