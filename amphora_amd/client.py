@@ -158,10 +158,35 @@ def create_masked_input(util: SecretShareUtil, secret: Secret,
 
 
 def _texts_and_words(bodies):
+    """Field texts of every party's body and the word count.  A malformed
+    body -- a field that is not a whole number of 16-byte words, or fields of
+    unequal length within or across parties -- is an AmphoraClientException,
+    as Jackson's deserialisation failure is in the reference
+    (DefaultAmphoraClient.java:206-217 via AmphoraCommunicationClient)."""
     from . import wire
     texts = [wire.odo_field_texts(b)[0] for b in bodies]
-    W = wire.words_of_b64(len(texts[0][0]), texts[0][0][-2:])
+    try:
+        W = wire.words_of_b64(len(texts[0][0]), texts[0][0][-2:])
+    except ValueError as e:
+        raise AmphoraClientException(str(e)) from e
+    n0 = len(texts[0][0])
+    if any(len(f) != n0 for t in texts for f in t):
+        # OutputDeliveryObject's constructor (OutputDeliveryObject.java:55-96)
+        raise AmphoraClientException("The provided shares must be of the same length")
     return texts, W
+
+
+def _wire_call(fn, *args, **kw):
+    """A fused wire-kernel call; a bad character or a length mismatch in some
+    party's text becomes AmphoraClientException."""
+    try:
+        return fn(*args, **kw)
+    except ValueError as e:  # an illegal base64 character in some party's body
+        raise AmphoraClientException(str(e)) from e
+    except _lib.AmphoraNativeError as e:
+        if e.status == _lib.AMPH_E_LEN:
+            raise AmphoraClientException(str(e)) from e
+        raise
 
 
 def _raise_for_texts(util: SecretShareUtil, texts, i: int):
@@ -170,22 +195,21 @@ def _raise_for_texts(util: SecretShareUtil, texts, i: int):
     _raise_for(util, arrays, i)
 
 
-def verify_vss_json(util: SecretShareUtil, bodies: Sequence[str]):
+def verify_vss_json(util: SecretShareUtil, bodies: Sequence[str], secret_id=None):
     """getSecret from the parties' VerifiableSecretShare JSON bodies
     (DefaultAmphoraClient.java:206-217 incl. Jackson's base64 decode of each
     field): the base64 member strings go to the fused K_RV wire kernel
     (amph_recombine_verify_b64) as they are.  Returns (secretId, tags,
-    canonical secrets) of the first body."""
+    canonical secrets).  As in the reference (:213-216) the secretId is the
+    one requested (`secret_id`; party 0's body only when none is given) and
+    only the tags come from party 0's body."""
     from . import wire
     texts, W = _texts_and_words(bodies)
-    try:
-        y, ff, _ = util.context.recombine_verify_b64(texts, W)
-    except ValueError as e:  # an illegal base64 character in some party's body
-        raise AmphoraClientException(str(e)) from e
+    y, ff, _ = _wire_call(util.context.recombine_verify_b64, texts, W)
     if ff >= 0:
         _raise_for_texts(util, texts, ff)
     sid, tags = wire.vss_metadata(bodies[0], wire.odo_field_texts(bodies[0])[1])
-    return sid, tags, unpack(y)
+    return (sid if secret_id is None else secret_id), tags, unpack(y)
 
 
 def create_masked_input_json(util: SecretShareUtil, secret: Secret, odo_bodies: Sequence[str]) -> str:
@@ -196,14 +220,12 @@ def create_masked_input_json(util: SecretShareUtil, secret: Secret, odo_bodies: 
     from . import wire
     texts, W = _texts_and_words(odo_bodies)
     if secret.size() > W:  # verify first, then the index error (as create_masked_input)
-        _, ff, _ = util.context.recombine_verify_b64(texts, W)
+        _, ff, _ = _wire_call(util.context.recombine_verify_b64, texts, W)
         if ff >= 0:
             _raise_for_texts(util, texts, ff)
         raise IndexError("Index %d out of bounds for length %d" % (W, W))
-    try:
-        _, rec, ff, _ = util.context.mask_input_b64(texts, W, pack(secret.data, util.prime), records=True)
-    except ValueError as e:
-        raise AmphoraClientException(str(e)) from e
+    _, rec, ff, _ = _wire_call(util.context.mask_input_b64, texts, W, pack(secret.data, util.prime),
+                               records=True)
     if ff >= 0:
         _raise_for_texts(util, texts, ff)
     return wire.records_to_masked_input_json(secret.secret_id, rec, secret.tags)

@@ -184,7 +184,7 @@ class LoopbackAmphoraClient:
             bodies = self._unwrap(self._fan_out(lambda p: wire.vss_to_json(
                 p.ctx, secret_id, p.secrets[secret_id].tags, p.get_secret_share(secret_id, request_id),
                 pretty=False)))
-            sid, tags, data = verify_vss_json(self.util, bodies)
+            sid, tags, data = verify_vss_json(self.util, bodies, secret_id)
             return Secret(sid, tags, data)
         odos = self._unwrap(self._fan_out(lambda p: p.get_secret_share(secret_id, request_id)))
         data = verify_output_delivery_objects(self.util, odos)

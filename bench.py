@@ -9,10 +9,14 @@ Inputs are synthetic honest N-party ODOs generated on the device (seeded),
 resident in HBM before the timed region.  Default workload = BASELINE config
 C2: 2^20 words per GPU, 2 parties, the reference's test prime.
 
-Multi-GPU (torchrun, one rank per GPU): each rank owns its own word shard
-(weak scaling, no data-path collective); the per-step verify verdicts are
-combined with one RCCL all-reduce(MIN) of the per-step first-fail vector
-after the last step.
+Multi-GPU (one rank per GPU): `--gpus N` under torch.distributed.run, or
+`--gpus N` alone, which starts torch.distributed.run itself as a child
+process before anything touches the GPU.  At N > 1 the default workload is
+BASELINE config C4: 2^26 words in total, 2 parties, one contiguous
+2^26 / N-word shard resident on each rank (strong scaling, no data-path
+collective); the per-step verify verdicts are combined with one RCCL
+all-reduce(MIN) of the per-step first-fail vector after the last step.
+`--workload c4` runs the same 2^26-word job at N = 1.
 
 Prints ONE JSON line (rank 0).  Per-kernel HIP-event timings on the launch
 stream (--samples launches of each kernel, spread over the timed steps) feed
@@ -61,10 +65,55 @@ def kbytes(kernel: str, n: int) -> int:
     return {"k_rv": 80 * n + 16, "k_mask": 80 * n + 32}[kernel]
 
 
+# BASELINE.json configs the device-resident bench runs: (words, parties,
+# words are per GPU (weak) or the whole job split over the ranks (strong))
+WORKLOADS = {"c2": (1 << 20, 2, "weak"), "c3": (1 << 24, 3, "weak"), "c4": (1 << 26, 2, "strong")}
+
+
 def config_name(words: int, parties: int) -> str:
     """BASELINE.json config a device-resident run corresponds to (per GPU)."""
     return {(1 << 20, 2): "C2", (1 << 24, 3): "C3", (1 << 26, 2): "C4 size"}.get(
         (words, parties), "custom")
+
+
+def available_cpus():
+    """CPUs this process may use: its affinity mask, capped by a cgroup-v2
+    CPU quota when one is set (a GPU box leases a share of a large host)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(a) -> int:
+    """`bench.py --gpus N` with no launcher: run N ranks under
+    torch.distributed.run as a CHILD process (nothing here has touched the
+    GPU, and nothing is exec'd), pass its one JSON line through, return its
+    exit code."""
+    import subprocess
+    argv = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            "--nproc-per-node", str(a.gpus), "--master-addr", "127.0.0.1",
+            "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(argv, env=env)
 
 
 def parse():
@@ -74,8 +123,16 @@ def parse():
     # steps take ~80 ms; host and scatter modes move GBs per step: 5 after 1
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
-    ap.add_argument("--words", type=int, default=1 << 20, help="words per GPU (C2: 2^20)")
-    ap.add_argument("--parties", type=int, default=2)
+    ap.add_argument("--workload", choices=["auto", "c2", "c3", "c4"], default="auto",
+                    help="device mode: BASELINE config; auto = C2 (2^20 words per GPU) at one "
+                         "rank, C4 (2^26 words split over the ranks) at several")
+    ap.add_argument("--words", type=int, default=None,
+                    help="words per GPU (custom device workload; host mode: words per rank; "
+                         "--scatter: total words)")
+    ap.add_argument("--parties", type=int, default=None)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher rehearsal without a GPU: rendezvous, shard ranges, the "
+                         "verdict and timing reductions over the process group; no kernels")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--samples", type=int, default=32,
                     help="event-stamped launches per kernel, spread evenly over the timed "
@@ -104,6 +161,18 @@ def parse():
                     help="C4: --words is the TOTAL array, held on rank 0 and scattered / "
                          "gathered over RCCL every step (strong scaling)")
     a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
+    if a.workload == "auto":
+        a.workload = "c2" if world == 1 else "c4"
+    wl_words, wl_parties, a.scaling = WORKLOADS[a.workload]
+    if a.words is None:
+        a.words = (1 << 20) if (a.mode == "host" or a.scatter) else wl_words
+    else:
+        a.workload, a.scaling = "custom", "weak"
+    if a.parties is None:
+        a.parties = 2 if (a.mode == "host" or a.scatter or a.workload == "custom") else wl_parties
+    elif a.parties != wl_parties and a.workload != "custom":
+        a.workload, a.scaling = "custom", "weak"
     bulk = a.mode == "host" or a.scatter
     if a.steps is None:
         a.steps = 5 if bulk else 1000
@@ -272,24 +341,35 @@ def host_mode(a, A, torch, ctx, dist=None, rank=0, world=1):
 def cpu_baseline(n: int, budget_s: float):
     """Time the C oracle (oracle/amphora_oracle.c: schoolbook multiply + Knuth
     division per fromGfp/toGfp, like BigInteger) on a bounded sample of the
-    same workload: K_MASK + K_RV arithmetic over W_s words, N parties."""
+    same workload: K_MASK + K_RV arithmetic over W_s words, N parties, on
+    every CPU the lease grants (affinity mask capped by the cgroup quota),
+    plus a short 1-thread pass for the per-core rate."""
     from oracle import coracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads, affinity, quota = available_cpus()
     F = coracle.test_field(threads=threads)
-    Ws = 1 << 16
+    Ws = max(1 << 16, min(1 << 20, 8192 * threads))  # ~ms of work per call at any thread count
     mask_odos, _ = F.synth_odos(seed=3, n=n, W=Ws)
     share_odos, _ = F.synth_odos(seed=4, n=n, W=Ws)
     secrets = F.synth_words(seed=5, count=Ws, mont=False)
-    F.mask_input(secrets, mask_odos)  # warm-up
-    done, t0 = 0, time.perf_counter()
-    while True:
-        _, f1 = F.mask_input(secrets, mask_odos)
-        _, f2 = F.recombine_verify(share_odos)
-        assert f1 == -1 and f2 == -1
-        done += Ws
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
+
+    def timed(budget, words):
+        sec = secrets[:words]
+        mo = [tuple(f[:words] for f in o) for o in mask_odos]
+        so = [tuple(f[:words] for f in o) for o in share_odos]
+        F.mask_input(sec, mo)  # warm-up
+        done, t0 = 0, time.perf_counter()
+        while True:
+            _, f1 = F.mask_input(sec, mo)
+            _, f2 = F.recombine_verify(so)
+            assert f1 == -1 and f2 == -1
+            done += words
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return done, el
+
+    done, el = timed(budget_s, Ws)
+    F.threads = 1
+    done1, el1 = timed(max(1.0, budget_s / 5), 4096)
     model = ""
     try:
         with open("/proc/cpuinfo") as fh:
@@ -297,10 +377,14 @@ def cpu_baseline(n: int, budget_s: float):
     except OSError:
         pass
     return {"value": done / el, "unit": "words/s", "cores": threads, "kind": "port",
-            "cpu_model": model, "host_cpus": os.cpu_count(),
+            "label": "C port of the BigInteger path (no JVM available)",
+            "value_1_thread": done1 / el1,
+            "cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
+            "cgroup_quota_cpus": quota,
             "sample": "%d words x %d reps (%.1f s): C oracle restating the Java BigInteger "
                       "path (maskInput+verify on %d-party mask ODOs, recombine+verify on "
-                      "share ODOs), OpenMP %d threads" % (Ws, done // Ws, el, n, threads)}
+                      "share ODOs), OpenMP %d threads; 1 thread: 4096 words x %d reps (%.1f s)"
+                      % (Ws, done // Ws, el, n, threads, done1 // 4096, el1)}
 
 
 def stream_probe_ms(lib, C, ctx, mask_arr, n, secrets, W, stream, samples, before):
@@ -379,22 +463,83 @@ def check_outputs(ctx, lib, torch, C, stream, flags, n, W, secrets, masked, ys, 
     return out
 
 
+def dry_run(a, world, rank):
+    """--dry-run: the multi-rank plumbing of the device bench with no GPU --
+    rendezvous, this rank's shard of the workload, the batched verdict
+    all-reduce(MIN) with local indices made global, the max-over-ranks time,
+    one line from rank 0.  `value` is null: nothing is measured."""
+    import torch
+    import torch.distributed as dist
+    from amphora_amd.shard import shard_range
+    if world > 1 or a.dist:
+        dist.init_process_group("gloo")
+    total = a.words if a.scaling == "strong" else a.words * world
+    start, count = shard_range(total, rank, world) if a.scaling == "strong" else (rank * a.words, a.words)
+    steps = a.warmup + a.steps
+    verdicts = torch.full((steps, 2), NO_FAIL, dtype=torch.int64)
+    if rank == world - 1:  # a fault in the last rank's shard, local index count // 3
+        verdicts[-1, 1] = count // 3
+    t0 = time.perf_counter()
+    verdicts = torch.where(verdicts == NO_FAIL, verdicts, verdicts + start)
+    if dist.is_initialized():
+        dist.all_reduce(verdicts, op=dist.ReduceOp.MIN)
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if dist.is_initialized():
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        sizes = torch.tensor([count], dtype=torch.int64)
+        dist.all_reduce(sizes)
+        covered = int(sizes.item())
+    else:
+        covered = count
+    if rank == 0:
+        emit({"metric": METRIC, "value": None, "unit": "words/s", "n_gpus": world, "dry_run": True,
+              "world_size": world, "backend": dist.get_backend() if dist.is_initialized() else None,
+              "scaling": a.scaling, "steps": a.steps, "warmup": a.warmup,
+              "words_covered": covered, "fault_reported_at": int(verdicts[-1, 1].item()),
+              "fault_expected_at": shard_range(total, world - 1, world)[0] + count // 3
+              if a.scaling == "strong" else (world - 1) * a.words + count // 3,
+              "config": workload_config(a, world)})
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def workload_config(a, world):
+    W, n = a.words, a.parties
+    if a.scaling == "strong":
+        name = "C4" if (W, n) == WORKLOADS["c4"][:2] else "custom"
+        return {"workload": "%s: K_MASK (share-encode) + K_RV (recombine+verify), %d words in total "
+                            "split into %d contiguous device-resident shards, %d parties, "
+                            "p = 2^127 < p < 2^128 test prime" % (name, W, world, n),
+                "words_total": W, "words_per_gpu": -(-W // world), "parties": n,
+                "parallelism": "dp%d" % world}
+    return {"workload": "%s: K_MASK (share-encode) + K_RV (recombine+verify), "
+                        "%d words per GPU, %d parties, p = 2^127 < p < 2^128 test prime"
+                        % (config_name(W, n), W, n),
+            "words_total": W * world, "words_per_gpu": W, "parties": n, "parallelism": "dp%d" % world}
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a))  # before anything initialises the GPU
     _claim_stdout()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if a.dry_run:
+        dry_run(a, world, rank)
+        return
     import torch
     import torch.distributed as dist
     import amphora_amd as A
     from amphora_amd.spdz import TEST_PRIME, TEST_R, TEST_RINV
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = 0 if a.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     distributed = world > 1 or a.dist
     if a.gpus != world and rank == 0:
-        print("bench.py: --gpus %d but WORLD_SIZE=%d; launch one process per GPU with "
-              "torch.distributed.run (measuring %d)" % (a.gpus, world, world), file=sys.stderr)
+        print("bench.py: --gpus %d but WORLD_SIZE=%d (measuring %d)" % (a.gpus, world, world),
+              file=sys.stderr)
     if distributed:
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -412,7 +557,14 @@ def main():
         if distributed:
             dist.destroy_process_group()
         return
-    W, n = a.words, a.parties
+    from amphora_amd.shard import shard_range
+    n = a.parties
+    if a.scaling == "strong":  # C4: this rank's contiguous shard of the whole job
+        start, W = shard_range(a.words, rank, world)
+        total_words = a.words
+    else:  # C2 / C3 / custom: W words on every rank
+        start, W = rank * a.words, a.words
+        total_words = a.words * world
     mask_odos, mbuf, mplain = ctx.synth_odos(seed=1000 + rank, n=n, words=W, with_plain=True)
     share_odos, sbuf, splain = ctx.synth_odos(seed=2000 + rank, n=n, words=W, with_plain=True)
     secrets = ctx.synth_words(seed=3000 + rank, count=W)
@@ -487,6 +639,8 @@ def main():
         jm, jr = mask_at.get(s), rv_at.get(s)
         step(ev_mask[jm] if jm is not None else None, ev_rv[jr] if jr is not None else None)
     if distributed:
+        if start:  # local first-fail indices -> global word indices
+            verdicts = torch.where(verdicts == NO_FAIL, verdicts, verdicts + start)
         dist.all_reduce(verdicts, op=dist.ReduceOp.MIN)  # per-step global verdicts
     torch.cuda.synchronize()
     if distributed:
@@ -525,7 +679,7 @@ def main():
 
     if rank == 0:
         ms = el * 1000.0 / a.steps
-        value = W * world * a.steps / el
+        value = total_words * a.steps / el
         kern = {"k_mask": t_mask, "k_rv": t_rv}
         dom = max(kern, key=kern.get)
         bpw = kbytes(dom, n)
@@ -541,12 +695,11 @@ def main():
         line = {
             "metric": METRIC, "value": value, "unit": "words/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u128 mod-p (4x u32 limbs)",
+            "scaling": a.scaling, "vs_baseline": None, "dtype": "u128 mod-p (4x u32 limbs)",
             "data": "synthetic: device-generated honest %d-party ODOs + secrets (seeded)" % n,
-            "config": {"workload": "%s: K_MASK (share-encode) + K_RV (recombine+verify), "
-                                   "%d words per GPU, %d parties, p = 2^127 < p < 2^128 test prime"
-                                   % (config_name(W, n), W, n),
-                       "words_per_gpu": W, "parties": n, "parallelism": "dp%d" % world},
+            "config": workload_config(a, world),
+            "world_size": world,
+            "backend": dist.get_backend() if distributed else None,
             "verified": ok,
             "verify_checks": checks,
             "kernels_ms": {k: round(v, 5) for k, v in kern.items()},

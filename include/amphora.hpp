@@ -296,7 +296,12 @@ inline std::vector<Bytes> maskSecret(const SecretShareUtil& util, const std::vec
 // uShares), kept as text: the client hands them to the fused wire kernels.
 struct OdoText {
   std::string f[5];
+  // amph_odo_b64 carries ONE length for the five fields: unequal fields are
+  // rejected here, before any copy reads them (OutputDeliveryObject.java:55-96).
   amph_odo_b64 view() const {
+    for (int k = 1; k < 5; ++k)
+      if (f[k].size() != f[0].size())
+        throw IllegalArgumentException("The provided shares must be of the same length");
     return amph_odo_b64{f[0].data(), f[1].data(), f[2].data(), f[3].data(), f[4].data(), f[0].size()};
   }
 };
@@ -349,6 +354,12 @@ inline std::vector<std::string> maskSecretText(const SecretShareUtil& util, cons
   std::vector<amph_odo_b64> v;
   for (auto& o : maskOdos) v.push_back(o.view());
   const size_t W = maskOdos.empty() ? 0 : wordsOfBase64(maskOdos[0].f[0]);
+  if (secret.size() > W) {
+    // the reference verifies every mask first (verifyOutputDeliveryObjects,
+    // DefaultAmphoraClient.java:153) and only then indexes past the masks (:155-157)
+    verifyOutputDeliveryText(util, maskOdos);
+    throw std::out_of_range("Index " + std::to_string(W) + " out of bounds for length " + std::to_string(W));
+  }
   std::vector<u128> s(secret);
   for (auto& x : s) x %= util.getPrime();
   Bytes in = packWords(s);

@@ -225,6 +225,38 @@ static void gpu_tests() {
     threw = std::string(e.what()).find("index 100 of party 0's vShares") != std::string::npos;
   }
   EXPECT(threw);
+  // one party's field shorter than its secretShares: rejected before any
+  // copy reads past it (host heap over-read otherwise)
+  auto shortField = texts;
+  shortField[1].f[2].resize(shortField[1].f[2].size() - 4);
+  for (int fn = 0; fn < 2; ++fn) {
+    threw = false;
+    try {
+      if (fn == 0) client::verifyOutputDeliveryText(util, shortField);
+      else client::maskSecretText(util, secrets, shortField);
+    } catch (const IllegalArgumentException& e) {
+      threw = std::string(e.what()) == "The provided shares must be of the same length";
+    }
+    EXPECT(threw);
+  }
+  // more secret words than masks: a tampered mask set fails verification
+  // first (DefaultAmphoraClient.java:153), an honest one the index check
+  std::vector<u128> longer(secrets);
+  longer.push_back(1);
+  threw = false;
+  try {
+    client::maskSecretText(util, longer, tamperedText);
+  } catch (const IntegrityVerificationException&) {
+    threw = true;
+  }
+  EXPECT(threw);
+  threw = false;
+  try {
+    client::maskSecretText(util, longer, texts);
+  } catch (const std::out_of_range&) {
+    threw = true;
+  }
+  EXPECT(threw);
 }
 
 int main(int argc, char** argv) {

@@ -76,3 +76,30 @@ def test_scatter_verify_gather_two_ranks(tmp_path, W, fault):
     ok, g, ref = open(tmp_path / "ok").read().split()
     assert ok == "1", (g, ref)
     assert int(g) == fault
+
+
+@pytest.mark.parametrize("extra,scaling,words", [([], "strong", 1 << 26),
+                                                  (["--workload", "c2"], "weak", 2 << 20)])
+def test_bench_spawns_ranks_itself(extra, scaling, words):
+    """`bench.py --gpus 2` with no launcher starts torch.distributed.run as a
+    child process (nothing touches a GPU first) and prints ONE JSON line from
+    rank 0: n_gpus 2, the C4 workload (2^26 words split into two shards) by
+    default at N > 1, and the verdict all-reduce turns rank 1's local fault
+    index into the global one.  --dry-run: the plumbing without kernels."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--same-device", "--dry-run"] + extra,
+                       capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["backend"] == "gloo"
+    assert line["scaling"] == scaling and line["words_covered"] == words
+    assert line["fault_reported_at"] == line["fault_expected_at"]
+    assert line["config"]["workload"].startswith("C4" if scaling == "strong" else "C2")

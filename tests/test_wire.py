@@ -618,3 +618,40 @@ def test_vss_json_tags_named_like_fields(ctx):
         sid2, tags2, odo2 = wire.vss_from_json(ctx, text)
         assert sid2 == sid and odo2 == odo
         assert [(t["key"], t["value"]) for t in tags2] == [(t["key"], t["value"]) for t in tags]
+
+
+def test_vss_json_malformed_fields_are_client_errors(ctx):
+    """A party body with a field that is not a whole number of words, or
+    with fields of unequal length, is an AmphoraClientException (ADVICE r2);
+    the secretId returned is the one requested (DefaultAmphoraClient.java:213-216)."""
+    import amphora_amd as A
+    from amphora_amd import client, wire
+    from oracle import coracle
+    F = coracle.test_field(threads=4)
+    util = client.SecretShareUtil.of(P, R, RINV)
+    odos, _ = F.synth_odos(seed=31, n=2, W=40)
+    sid = uuid.UUID("80fbba1b-3da8-4b1e-8a2c-cebd65229fad")
+    asked = uuid.UUID("00000000-0000-4000-8000-000000000001")
+    names = ("secretShares", "rShares", "vShares", "wShares", "uShares")
+
+    def bodies(cut=None):  # cut(j, k) -> bytes to drop from party j's field k
+        out = []
+        for j, o in enumerate(odos):
+            f = [bytes(np.ascontiguousarray(x).tobytes()) for x in o]
+            d = json.loads(wire.vss_to_json(ctx, sid, [], A.OutputDeliveryObject(*f), pretty=False))
+            for k in range(5):
+                c = cut(j, k) if cut else 0
+                if c:
+                    d[names[k]] = base64.b64encode(f[k][:-c]).decode()
+            out.append(json.dumps(d, separators=(",", ":")))
+        return out
+
+    got_sid, _, ys = client.verify_vss_json(util, bodies(), asked)
+    assert got_sid == asked
+    assert ys == [int.from_bytes(w.tobytes(), "little") for w in F.recombine_verify(odos)[0]]
+    with pytest.raises(A.AmphoraClientException):  # 15 bytes short of a whole word
+        client.verify_vss_json(util, bodies(lambda j, k: 1 if j == 0 else 0))
+    with pytest.raises(A.AmphoraClientException, match="same length"):
+        client.verify_vss_json(util, bodies(lambda j, k: 16 if (j, k) == (1, 2) else 0))
+    with pytest.raises(A.AmphoraClientException):  # one whole party a word short
+        client.verify_vss_json(util, bodies(lambda j, k: 16 if j == 1 else 0))
