@@ -126,6 +126,12 @@ struct amph_ctx {
   DevBuf xstage;  // host-mode staging of the exchange codec calls
   DevBuf xdev;    // device-mode scan scratch of the exchange codec calls
   hipEvent_t xdev_done = nullptr;  // the last device-mode exchange call's kernels
+  // small host calls (run_small): one page-locked arena the kernels read and
+  // write in place, and device verdict words kept at kNoFail between calls
+  size_t small_bytes = (size_t)2 << 20;
+  amph::PinnedBuf small;
+  DevBuf small_ff;
+  bool small_ff_dirty = true;
   std::unique_ptr<amph::CopyPool> pool;
 };
 
@@ -200,10 +206,30 @@ struct HostOut {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// kPageableRule -- the ordering rule every host<->device copy here follows:
+//
+//   hipMemcpyAsync is used ONLY with page-locked host memory (the batched
+//   pipeline's slot buffers, or caller buffers is_pinned_host() reports as
+//   registered).  Pageable host memory moves with a blocking hipMemcpy,
+//   issued only once the context stream that produces / consumes the device
+//   side has been synchronised.
+//
+// Why: HIP defines an async copy of pageable memory only as "performed
+// synchronously" (hip_runtime_api.h, hipMemcpyAsync @note) -- a host-staged
+// transfer, not the stream-ordered copy CUDA code assumes -- so its order
+// against the kernels of a non-blocking stream is not a guarantee this
+// library may build on.  Round 2 saw that order fail once in each direction,
+// both times in a one-shot call on a non-blocking context stream:
+//   * DtoH (1e4fc5f): a pageable verdict word on the stack, hipMemcpyAsync'd
+//     after the kernel that writes it, held the value from before the kernel;
+//   * HtoD (9513c3e): base64 text hipMemcpyAsync'd from pageable memory into
+//     hipMallocAsync staging on the same stream was seen by the kernel with
+//     its first 16-character unit (the head of the first copy) unwritten.
+// tests/test_host_ordering.py checks the rule statically over this file and
+// runs a fresh process's first wire-text calls on the GPU.
+//
 // Results of a one-shot host call: wait for the stream, then copy with
-// blocking hipMemcpy.  (A small hipMemcpyAsync into pageable host memory --
-// a verdict word on the stack -- was once seen to hold a value from before
-// the kernel on the same stream; the copies below cannot.)
+// blocking hipMemcpy.
 struct ReadBack {
   void* dst;
   const void* src;
@@ -387,6 +413,114 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
   return AMPH_OK;
 }
 
+// ---- small host calls ------------------------------------------------------------
+// A host call whose inputs and outputs together fit c->small_bytes (default
+// 2 MiB; AMPH_SMALL_BYTES, 0 = off) skips the batched pipeline: the inputs
+// are memcpy'd into the context's page-locked arena, the kernel reads them
+// and writes its outputs there in place (hipHostMalloc memory is mapped into
+// the device's address space), its verdict words go from device memory to
+// the arena by one 64-lane copy kernel, and the call makes ONE stream
+// synchronisation -- no DMA round trips, events or staging threads.  At C1
+// sizes (1 k words) each host call is then launch + PCIe latency, where the
+// batched path paid three streams' worth of copies and synchronisations.
+// Kernel stores to the arena are visible to the host once the stream has
+// synchronised (end-of-kernel system-scope release); the CPU's memcpy into
+// it completes before the launch is issued.
+struct Arena {
+  uint8_t* base = nullptr;
+  size_t off = 0;
+  uint8_t* take(size_t bytes) {
+    uint8_t* p = base + off;
+    off += align256(bytes ? bytes : 16);
+    return p;
+  }
+};
+
+int host_stream1(amph_ctx* c, hipStream_t* s) {
+  if (!c->streams[1]) HIP_TRY(hipStreamCreateWithFlags(&c->streams[1], hipStreamNonBlocking));
+  *s = c->streams[1];
+  return AMPH_OK;
+}
+
+bool small_call(const amph_ctx* c, size_t bytes) { return c->small_bytes && bytes <= c->small_bytes; }
+
+// `bytes` of arena (plus 256 for the verdict words at its head) and the
+// device verdict words, reset if an earlier call left them unknown
+int small_begin(amph_ctx* c, size_t bytes, hipStream_t s, Arena* a, unsigned long long** dff) {
+  if (c->small.ensure(bytes + 256) != hipSuccess) return fail(AMPH_E_NOMEM, "small-call arena");
+  if (c->small_ff.ensure(256) != hipSuccess) return fail(AMPH_E_NOMEM, "small-call verdict words");
+  if (c->small_ff_dirty) {
+    HIP_TRY(hipMemsetAsync(c->small_ff.p, 0x7F, 256, s));
+    c->small_ff_dirty = false;
+  }
+  a->base = (uint8_t*)c->small.p;
+  a->off = 256;
+  *dff = (unsigned long long*)c->small_ff.p;
+  return AMPH_OK;
+}
+
+// after the kernels: verdict words to the arena head, one synchronisation
+int small_end(amph_ctx* c, hipStream_t s, int n_ff) {
+  hipError_t e = amph::launch_take_words((unsigned long long*)c->small_ff.p, (unsigned long long*)c->small.p,
+                                         n_ff, s);
+  if (e != hipSuccess) {
+    c->small_ff_dirty = true;
+    (void)hipStreamSynchronize(s);
+    return hip_fail(e, "verdict copy");
+  }
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    c->small_ff_dirty = true;
+    return hip_fail(e, "small-call synchronise");
+  }
+  return AMPH_OK;
+}
+
+int small_launch_failed(amph_ctx* c, hipStream_t s, hipError_t e, const char* what) {
+  c->small_ff_dirty = true;
+  (void)hipStreamSynchronize(s);
+  return hip_fail(e, what);
+}
+
+template <class Launch>
+int run_small(amph_ctx* c, size_t words, const std::vector<HostIn>& ins, const std::vector<HostOut>& outs,
+              bool with_ff, int64_t* first_fail, Launch& launch, size_t bytes) {
+  if (first_fail) *first_fail = -1;
+  if (words == 0) return AMPH_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s;
+  if (int st = host_stream1(c, &s)) return st;
+  Arena a;
+  unsigned long long* dff;
+  if (int st = small_begin(c, bytes, s, &a, &dff)) return st;
+  std::vector<const uint4*> din;
+  std::vector<uint4*> dout;
+  for (const HostIn& x : ins) {
+    uint8_t* p = a.take(words * x.bytes_per_word);
+    std::memcpy(p, x.host, words * x.bytes_per_word);
+    din.push_back((const uint4*)p);
+  }
+  for (const HostOut& x : outs) dout.push_back((uint4*)a.take(words * x.bytes_per_word));
+  hipError_t e = launch(din, dout, words, with_ff ? dff : nullptr, cfg(c, s, words));
+  if (e != hipSuccess) return small_launch_failed(c, s, e, "kernel launch");
+  if (int st = small_end(c, s, with_ff ? 1 : 0)) return st;
+  for (size_t k = 0; k < outs.size(); ++k)
+    std::memcpy(outs[k].host, dout[k], words * outs[k].bytes_per_word);
+  const unsigned long long v = *(volatile unsigned long long*)c->small.p;
+  if (with_ff && v != amph::kNoFail) {
+    if (first_fail) *first_fail = (int64_t)v;
+    return AMPH_E_VERIFY;
+  }
+  return AMPH_OK;
+}
+
+size_t call_bytes(size_t words, const std::vector<HostIn>& ins, const std::vector<HostOut>& outs) {
+  size_t b = 0;
+  for (const HostIn& x : ins) b += align256(words * x.bytes_per_word);
+  for (const HostOut& x : outs) b += align256(words * x.bytes_per_word);
+  return b;
+}
+
 // An error part-way through leaves earlier batches' copies in flight (into
 // the caller's page-locked buffers, or the slots): wait for them before
 // returning, so nothing writes caller memory after the call has returned.
@@ -395,6 +529,8 @@ int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
                 const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
                 Launch&& launch, size_t ff_scale = 1) {
   if (!c->sub.empty()) return run_sharded(c, words, ins, outs, with_ff, first_fail, launch, ff_scale);
+  const size_t bytes = call_bytes(words, ins, outs);
+  if (small_call(c, bytes)) return run_small(c, words, ins, outs, with_ff, first_fail, launch, bytes);
   const int rc = run_batched_impl(c, words, ins, outs, with_ff, first_fail, launch, ff_scale);
   if (rc != AMPH_OK && rc != AMPH_E_VERIFY) {
     for (int s = 0; s < amph_ctx::kSlots; ++s) {
@@ -576,6 +712,7 @@ int amph_ctx_create(const uint8_t p_le[16], const uint8_t r_le[16], const uint8_
   }
   c->device = device;
   if (const char* g = std::getenv("AMPH_GRID_CAP")) c->grid_cap = std::max(0, std::atoi(g));
+  if (const char* sb = std::getenv("AMPH_SMALL_BYTES")) c->small_bytes = (size_t)std::strtoull(sb, nullptr, 10);
   if (const char* b = std::getenv("AMPH_BLOCK")) {
     const int v = std::atoi(b);
     if (v >= 64 && v <= amph::kMaxBlock && v % 64 == 0) c->block = v;
@@ -627,6 +764,12 @@ void amph_ctx_destroy(amph_ctx* c) {
     c->tail.release();
     c->wire.release();
     c->xstage.release();
+  }
+  if (c->small.p || c->small_ff.p) {
+    (void)hipSetDevice(c->device);
+    if (c->streams[1]) (void)hipStreamSynchronize(c->streams[1]);
+    c->small.release();
+    c->small_ff.release();
   }
   if (c->xdev_done) {
     (void)hipSetDevice(c->device);
@@ -1036,7 +1179,10 @@ int run_tail(amph_ctx* c, const void* in, size_t in_bytes, void* out, size_t out
   if (!c->streams[0]) HIP_TRY(hipStreamCreateWithFlags(&c->streams[0], hipStreamNonBlocking));
   hipStream_t s = c->streams[0];  // the context's own stream: no device-wide sync
   uint8_t* d = (uint8_t*)c->tail.p;
-  HIP_TRY(hipMemcpyAsync(d, in, in_bytes, hipMemcpyHostToDevice, s));
+  // `in` is caller memory, pageable in general: a blocking copy after the
+  // stream is idle (kPageableRule, above read_back)
+  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(hipMemcpy(d, in, in_bytes, hipMemcpyHostToDevice));
   if (with_bad) HIP_TRY(hipMemsetAsync(d + 448, 0x7F, 8, s));
   e = launch(d, d + 256, (unsigned long long*)(d + 448), cfg(c, s, 1));
   if (e != hipSuccess) return hip_fail(e, "codec tail");
@@ -1246,6 +1392,32 @@ int amph_exchange_encode(amph_ctx* c, const uint8_t* mag16, const uint8_t* neg, 
     return AMPH_OK;
   }
   std::lock_guard<std::mutex> g(c->mu);
+  if (npairs && small_call(c, align256(32 * npairs) + align256(2 * npairs) + align256(maxb))) {
+    // small call: diffs in, text out through the page-locked arena, one sync
+    hipStream_t s;
+    if (int st = host_stream1(c, &s)) return st;
+    Arena a;
+    unsigned long long* dff;
+    if (int st = small_begin(c, align256(32 * npairs) + align256(2 * npairs) + align256(maxb), s, &a, &dff))
+      return st;
+    XStage x;
+    const size_t ssz[1] = {amph::xenc_scratch_bytes(npairs)};
+    if (int st = x.stage(c, ssz, 1)) return st;
+    uint8_t *hmag = a.take(32 * npairs), *hneg = a.take(2 * npairs), *htext = a.take(maxb);
+    std::memcpy(hmag, mag16, 32 * npairs);
+    std::memcpy(hneg, neg, 2 * npairs);
+    unsigned long long* hlen = (unsigned long long*)c->small.p;  // the arena head
+    hipError_t e = amph::launch_exchange_encode((const uint4*)hmag, hneg, npairs, (char*)htext, hlen,
+                                                x.take(ssz[0]), cfg(c, s, npairs));
+    if (e != hipSuccess) return small_launch_failed(c, s, e, "k_xenc");
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint64_t len = *(volatile unsigned long long*)hlen;
+    *out_len = len;
+    if (len > out_cap) return fail(AMPH_E_LEN, "output capacity " + std::to_string(out_cap) +
+                                                   " below the encoded length " + std::to_string(len));
+    std::memcpy(out, htext, len);
+    return AMPH_OK;
+  }
   hipStream_t s;
   if (int st = host_stream0(c, &s)) return st;
   XStage x;
@@ -1289,6 +1461,35 @@ int amph_exchange_decode(amph_ctx* c, const char* text, size_t len, size_t npair
     return AMPH_OK;
   }
   std::lock_guard<std::mutex> g(c->mu);
+  const size_t sbytes = align256(len) + align256(32 * npairs) + align256(2 * npairs);
+  if (len && small_call(c, sbytes)) {
+    // small call: text in, diffs out through the page-locked arena, one sync
+    hipStream_t s;
+    if (int st = host_stream1(c, &s)) return st;
+    Arena a;
+    unsigned long long* dff;
+    if (int st = small_begin(c, sbytes, s, &a, &dff)) return st;
+    XStage x;
+    const size_t ssz[1] = {amph::xdec_scratch_bytes(len)};
+    if (int st = x.stage(c, ssz, 1)) return st;
+    uint8_t *htext = a.take(len), *hmag = a.take(32 * npairs), *hneg = a.take(2 * npairs);
+    std::memcpy(htext, text, len);
+    hipError_t e = amph::launch_exchange_decode((const char*)htext, len, npairs, (uint4*)hmag, hneg, dff,
+                                                x.take(ssz[0]), cfg(c, s, len));
+    if (e != hipSuccess) return small_launch_failed(c, s, e, "k_xdec");
+    if (int st = small_end(c, s, 1)) return st;
+    const int64_t bad = (int64_t) * (volatile unsigned long long*)c->small.p;
+    const bool ok = bad == (int64_t)AMPH_NO_FAILURE;
+    if (bad_index) *bad_index = ok ? -1 : bad;
+    if (!ok) {
+      if ((size_t)bad == len)
+        return fail(AMPH_E_LEN, "interimValues must hold exactly " + std::to_string(npairs) + " FactorPairs");
+      return fail(AMPH_E_PARAM, "Malformed FactorPair JSON at offset " + std::to_string(bad));
+    }
+    std::memcpy(mag16, hmag, 32 * npairs);
+    std::memcpy(neg, hneg, 2 * npairs);
+    return AMPH_OK;
+  }
   hipStream_t s;
   if (int st = host_stream0(c, &s)) return st;
   XStage x;
@@ -1353,16 +1554,20 @@ int wire_bad_message(int64_t bad, size_t nchars) {
                                 std::to_string(o / 5) + "'s " + kOdoFieldNames[o % 5]);
 }
 
-// Host mode: the texts go to the device in one blocking copy each into the
-// context's staging buffer (no batching: the whole call is one launch), the
-// kernel runs on the context's stream, and the results come back after it.
-// (A first version staged through stream-ordered hipMallocAsync memory with
-// pageable hipMemcpyAsync; in a fresh process its first call intermittently
-// saw the first text unit unwritten.)
+// Host mode, one launch per call (no batching).  Small calls (c->small_bytes)
+// stage the texts in the page-locked arena, which the kernel reads in place,
+// and make one stream synchronisation (run_small).  Larger ones copy each
+// text with a blocking hipMemcpy into the context's device staging buffer
+// (kPageableRule), run the kernel on the context's stream, and read the
+// results back after it.  (A first version staged through stream-ordered
+// hipMallocAsync memory with pageable hipMemcpyAsync; in a fresh process its
+// first call intermittently saw the first text unit unwritten.)
 struct WireHost {
   amph::TextSet tx{};
   uint8_t* base = nullptr;
   size_t off = 0;
+  bool small = false;
+  unsigned long long* fl = nullptr;  // first-fail, bad character
   uint8_t* take(size_t bytes) {
     uint8_t* p = base + off;
     off += align256(bytes ? bytes : 16);
@@ -1371,17 +1576,54 @@ struct WireHost {
   static size_t bytes_for(int n, size_t nchars, size_t extra) {
     return 5 * n * align256(nchars ? nchars : 16) + extra + 256;
   }
-  int stage(amph_ctx* c, const amph_odo_b64* odos, int n, size_t nchars, size_t extra) {
-    hipError_t e = c->wire.ensure(bytes_for(n, nchars, extra));
-    if (e != hipSuccess) return fail(AMPH_E_NOMEM, "wire staging");
-    base = (uint8_t*)c->wire.p;
+  int stage(amph_ctx* c, const amph_odo_b64* odos, int n, size_t nchars, size_t extra, hipStream_t s) {
+    const size_t bytes = bytes_for(n, nchars, extra);
+    small = small_call(c, bytes);
+    if (small) {
+      Arena a;
+      if (int st = small_begin(c, bytes, s, &a, &fl)) return st;
+      base = a.base;
+      off = a.off;
+    } else {
+      hipError_t e = c->wire.ensure(bytes);
+      if (e != hipSuccess) return fail(AMPH_E_NOMEM, "wire staging");
+      base = (uint8_t*)c->wire.p;
+    }
     for (int j = 0; j < n; ++j)
       for (int k = 0; k < 5; ++k) {
         uint8_t* d = take(nchars);
-        if (nchars) HIP_TRY(hipMemcpy(d, b64_field(odos[j], k), nchars, hipMemcpyHostToDevice));
+        if (nchars) HIP_TRY(put(d, b64_field(odos[j], k), nchars));
         tx.t[k][j] = (const char*)d;
       }
+    if (!small) {
+      fl = (unsigned long long*)take(16);
+      HIP_TRY(hipMemsetAsync(fl, 0x7F, 16, s));
+    }
     return AMPH_OK;
+  }
+  hipError_t put(void* dst, const void* src, size_t bytes) {
+    if (small) {
+      std::memcpy(dst, src, bytes);
+      return hipSuccess;
+    }
+    return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+  }
+  // after the launch: the two verdict words and the outputs to the caller
+  int finish(amph_ctx* c, hipStream_t s, int64_t v[2], std::initializer_list<ReadBack> outs) {
+    if (small) {
+      if (int st = small_end(c, s, 2)) return st;
+      std::memcpy(v, c->small.p, 16);
+      for (const ReadBack& r : outs)
+        if (r.bytes) std::memcpy(r.dst, r.src, r.bytes);
+      return AMPH_OK;
+    }
+    HIP_TRY(read_back(s, {{v, fl, 16}}));
+    for (const ReadBack& r : outs)
+      if (r.bytes) HIP_TRY(hipMemcpy(r.dst, r.src, r.bytes, hipMemcpyDeviceToHost));
+    return AMPH_OK;
+  }
+  int launch_failed(amph_ctx* c, hipStream_t s, hipError_t e, const char* what) {
+    return small ? small_launch_failed(c, s, e, what) : hip_fail(e, what);
   }
 };
 }  // namespace
@@ -1418,15 +1660,13 @@ int amph_recombine_verify_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size
   hipStream_t s;
   if (int st = host_stream0(c, &s)) return st;
   WireHost h;
-  if (int st = h.stage(c, odos, n, nchars, align256(16 * words) + 256)) return st;
+  if (int st = h.stage(c, odos, n, nchars, align256(16 * words) + 256, s)) return st;
   uint8_t* dout = h.take(16 * words);
-  unsigned long long* fl = (unsigned long long*)h.take(16);
-  HIP_TRY(hipMemsetAsync(fl, 0x7F, 16, s));
-  hipError_t e = amph::launch_rv_b64(h.tx, n, words, nchars, pad, (uint4*)dout, fl, fl + 1, c->f,
+  hipError_t e = amph::launch_rv_b64(h.tx, n, words, nchars, pad, (uint4*)dout, h.fl, h.fl + 1, c->f,
                                      cfg(c, s, words));
-  if (e != hipSuccess) return hip_fail(e, "k_rv_b64");
+  if (e != hipSuccess) return h.launch_failed(c, s, e, "k_rv_b64");
   int64_t v[2];
-  HIP_TRY(read_back(s, {{v, fl, 16}, {out_secrets, dout, 16 * words}}));
+  if (int st = h.finish(c, s, v, {{out_secrets, dout, 16 * words}})) return st;
   if (v[1] != (int64_t)AMPH_NO_FAILURE) {
     if (bad_char) *bad_char = v[1];
     return wire_bad_message(v[1], nchars);
@@ -1472,20 +1712,19 @@ int amph_mask_input_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size_t wor
   if (int st = host_stream0(c, &s)) return st;
   WireHost h;
   const size_t extra = 3 * align256(16 * n_secrets) + align256(24 * n_secrets) + 1024;
-  if (int st = h.stage(c, odos, n, nchars, extra)) return st;
+  if (int st = h.stage(c, odos, n, nchars, extra, s)) return st;
   uint8_t* dsec = h.take(16 * n_secrets);
   uint8_t* d16 = h.take(16 * n_secrets);
   uint8_t* d24 = h.take(24 * n_secrets);
-  unsigned long long* fl = (unsigned long long*)h.take(16);
-  if (n_secrets) HIP_TRY(hipMemcpy(dsec, secrets, 16 * n_secrets, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemsetAsync(fl, 0x7F, 16, s));
+  if (n_secrets) HIP_TRY(h.put(dsec, secrets, 16 * n_secrets));
   hipError_t e = amph::launch_mask_b64(h.tx, n, words, nchars, pad, (const uint4*)dsec, n_secrets,
                                        out16 ? (uint4*)d16 : nullptr, out24 ? (char*)d24 : nullptr,
-                                       fl, fl + 1, c->f, cfg(c, s, words));
-  if (e != hipSuccess) return hip_fail(e, "k_mask_b64");
+                                       h.fl, h.fl + 1, c->f, cfg(c, s, words));
+  if (e != hipSuccess) return h.launch_failed(c, s, e, "k_mask_b64");
   int64_t v[2];
-  HIP_TRY(read_back(s, {{v, fl, 16}, {out16, d16, out16 ? 16 * n_secrets : 0},
-                        {out24, d24, out24 ? 24 * n_secrets : 0}}));
+  if (int st = h.finish(c, s, v, {{out16, d16, out16 ? 16 * n_secrets : 0},
+                                  {out24, d24, out24 ? 24 * n_secrets : 0}}))
+    return st;
   if (v[1] != (int64_t)AMPH_NO_FAILURE) {
     if (bad_char) *bad_char = v[1];
     return wire_bad_message(v[1], nchars);

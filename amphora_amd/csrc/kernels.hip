@@ -980,6 +980,25 @@ hipError_t launch_stream_probe(const OdoSet& odo, int n, size_t words, const uin
   return hipGetLastError();
 }
 
+namespace {
+// Small host calls (capi.hip run_small): the verdict words the kernels
+// atomicMin'd into device memory go to the page-locked staging arena with
+// plain vector stores, and are reset to kNoFail for the next call.
+__global__ void k_take_words(unsigned long long* dev, unsigned long long* host, int n) {
+  const int i = threadIdx.x;
+  if (i < n) {
+    host[i] = dev[i];
+    dev[i] = kNoFail;
+  }
+}
+}  // namespace
+
+hipError_t launch_take_words(unsigned long long* dev, unsigned long long* host, int n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_take_words, dim3(1), dim3(64), 0, s, dev, host, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_synth_words(uint4* out, size_t count, uint64_t seed, const Fp& f,
                               const LaunchCfg& c) {
   if (count == 0) return hipSuccess;

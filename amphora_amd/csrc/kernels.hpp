@@ -132,6 +132,10 @@ hipError_t launch_mask_b64(const TextSet& tx, int n, size_t words, size_t nchars
                            unsigned long long* first_fail, unsigned long long* bad, const Fp& f,
                            const LaunchCfg& c);
 
+// Small host calls: copy n verdict words from device memory to page-locked
+// host memory and reset them to kNoFail (one 64-lane workgroup).
+hipError_t launch_take_words(unsigned long long* dev, unsigned long long* host, int n, hipStream_t s);
+
 // Measurement only: K_MASK's memory pattern without the arithmetic.
 hipError_t launch_stream_probe(const OdoSet& odo, int n, size_t words, const uint4* secrets,
                                uint4* out, const LaunchCfg& c);

@@ -24,6 +24,10 @@ run_all() {
   step bench_c2 300 python3 bench.py || return
   step bench_c4_n1 300 python3 bench.py --workload c4 --no-cpu-baseline || return
   step bench_c4_gloo2 300 python3 bench.py --gpus 2 --backend gloo --same-device || return
+  step c1_own 120 ./tools/c1_native 1024 30 own || return
+  step c1_shared 120 ./tools/c1_native 1024 30 shared || return
+  step c1_own_4k 120 ./tools/c1_native 4096 20 own || return
+  step c1_own_64k 120 ./tools/c1_native 65536 10 own || return
 }
 run_all
 rc=$?
