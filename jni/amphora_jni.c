@@ -1,0 +1,427 @@
+/*
+ * libamphora_jni: the JNI layer between the Java drop-ins under java/ and
+ * libamphora_hip (include/amphora.h).  It only pins Java arrays and maps
+ * statuses to exceptions; lengths are checked and the C ABI is called by the
+ * JNI-independent core (amphora_jni_core.c, tested without a JDK by
+ * tests/test_jni_core.py).
+ *
+ *   io.carbynestack.amphora.client.NativeShareArithmetic
+ *     <- client SecretShareUtil.java:48-141, DefaultAmphoraClient.java:150-217,476-505
+ *   io.carbynestack.amphora.service.calculation.NativeShareArithmetic
+ *     <- service SecretShareUtil.java:58-107, OutputDeliveryService.java:75-286
+ *
+ * Pinning: GetPrimitiveArrayCritical; inside a critical region a thread may
+ * make no JNI call but further Get/ReleasePrimitiveArrayCritical, so every
+ * array element and length is fetched before the first array is pinned.  A
+ * verify failure is RETURNED (the smallest failing word index); the Java side
+ * builds the IntegrityVerificationException message from that word's values,
+ * as SecretShareUtil.java:116-129 does.  Other failures are thrown here:
+ * IllegalArgumentException for length / argument errors (the reference's
+ * messages where it has one), IllegalStateException for runtime errors.
+ *
+ * Build: jni/Makefile (skipped when no JDK is found -- this image has none).
+ */
+#include <jni.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "amphora_jni_core.h"
+
+#define MAXP AMPH_MAX_PARTIES
+
+typedef struct {
+  jbyteArray ref;
+  jsize len;
+  jbyte* p;
+} Pin;
+
+static void throw_status(JNIEnv* env, int status) {
+  const char* cls = amphj_exception_class(status);
+  jclass c = cls ? (*env)->FindClass(env, cls) : NULL;
+  if (c) (*env)->ThrowNew(env, c, amphj_message());
+}
+
+static int throw_arg(JNIEnv* env, const char* msg) {
+  jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+  if (c) (*env)->ThrowNew(env, c, msg);
+  return -1;
+}
+
+/* refs + lengths of one array (null allowed only when `optional`) */
+static int ref(JNIEnv* env, jbyteArray a, Pin* p) {
+  if (!a) return throw_arg(env, "null array");
+  p->ref = a;
+  p->len = (*env)->GetArrayLength(env, a);
+  p->p = NULL;
+  return 0;
+}
+
+/* byte[][] fields (one per party) of k = 0..4 into pins[k * n + j] */
+static int refs_odo(JNIEnv* env, jobjectArray f[5], Pin* pins, int* n) {
+  for (int k = 0; k < 5; ++k)
+    if (!f[k]) return throw_arg(env, "null ODO field list");
+  *n = (*env)->GetArrayLength(env, f[0]);
+  if (*n < 1 || *n > MAXP) return throw_arg(env, "n_parties must be in [1, 16]");
+  for (int k = 0; k < 5; ++k) {
+    if ((*env)->GetArrayLength(env, f[k]) != *n)
+      return throw_arg(env, "The provided shares must be of the same length");
+    for (int j = 0; j < *n; ++j)
+      if (ref(env, (jbyteArray)(*env)->GetObjectArrayElement(env, f[k], j), &pins[k * *n + j])) return -1;
+  }
+  return 0;
+}
+
+static int refs_list(JNIEnv* env, jobjectArray a, Pin* pins, int* n) {
+  if (!a) return throw_arg(env, "null array list");
+  *n = (*env)->GetArrayLength(env, a);
+  if (*n < 1 || *n > MAXP) return throw_arg(env, "n_parties must be in [1, 16]");
+  for (int j = 0; j < *n; ++j)
+    if (ref(env, (jbyteArray)(*env)->GetObjectArrayElement(env, a, j), &pins[j])) return -1;
+  return 0;
+}
+
+static void pin_all(JNIEnv* env, Pin* pins, int count) {
+  for (int i = 0; i < count; ++i) pins[i].p = (*env)->GetPrimitiveArrayCritical(env, pins[i].ref, NULL);
+}
+
+/* outputs (written) are committed, inputs aborted (never copied back) */
+static void unpin_all(JNIEnv* env, Pin* pins, int count, int first_output) {
+  for (int i = count - 1; i >= 0; --i)
+    if (pins[i].p)
+      (*env)->ReleasePrimitiveArrayCritical(env, pins[i].ref, pins[i].p, i >= first_output ? 0 : JNI_ABORT);
+}
+
+static void ptrs_of(const Pin* pins, int count, const uint8_t** ptrs, size_t* lens) {
+  for (int i = 0; i < count; ++i) {
+    ptrs[i] = (const uint8_t*)pins[i].p;
+    lens[i] = (size_t)pins[i].len;
+  }
+}
+
+static jlong ctx_create(JNIEnv* env, jbyteArray p, jbyteArray r, jbyteArray rinv, jintArray devices) {
+  Pin a[3];
+  if (ref(env, p, &a[0]) || ref(env, r, &a[1]) || ref(env, rinv, &a[2])) return 0;
+  jint dev[MAXP];
+  int ndev = 0;
+  if (devices) {
+    ndev = (*env)->GetArrayLength(env, devices);
+    if (ndev > MAXP) return throw_arg(env, "at most 16 devices"), 0;
+    (*env)->GetIntArrayRegion(env, devices, 0, ndev, dev);
+  }
+  jbyte b[3][16];
+  for (int i = 0; i < 3; ++i) {
+    if (a[i].len != 16) return throw_arg(env, "prime, r and rInv must be 16-byte little-endian integers"), 0;
+    (*env)->GetByteArrayRegion(env, a[i].ref, 0, 16, b[i]);
+  }
+  void* ctx = NULL;
+  const int st = amphj_ctx_create((const uint8_t*)b[0], 16, (const uint8_t*)b[1], 16, (const uint8_t*)b[2], 16,
+                                  dev, ndev, &ctx);
+  if (st != AMPH_OK) {
+    throw_status(env, st);
+    return 0;
+  }
+  return (jlong)(intptr_t)ctx;
+}
+
+#define CTX(x) ((void*)(intptr_t)(x))
+
+/* ---- client ------------------------------------------------------------------- */
+#define CLIENT(name) Java_io_carbynestack_amphora_client_NativeShareArithmetic_##name
+
+JNIEXPORT jlong JNICALL CLIENT(ctxCreate)(JNIEnv* env, jclass cls, jbyteArray p, jbyteArray r, jbyteArray rinv,
+                                          jintArray devices) {
+  (void)cls;
+  return ctx_create(env, p, r, rinv, devices);
+}
+
+JNIEXPORT void JNICALL CLIENT(ctxDestroy)(JNIEnv* env, jclass cls, jlong ctx) {
+  (void)env;
+  (void)cls;
+  amphj_ctx_destroy(CTX(ctx));
+}
+
+/* DefaultAmphoraClient.verifyOutputDeliveryObjects :476-505 -> -1 or the failing word */
+JNIEXPORT jlong JNICALL CLIENT(recombineVerify)(JNIEnv* env, jclass cls, jlong ctx, jobjectArray y,
+                                                jobjectArray r, jobjectArray v, jobjectArray w, jobjectArray u,
+                                                jbyteArray out) {
+  (void)cls;
+  jobjectArray f[5] = {y, r, v, w, u};
+  Pin pins[5 * MAXP + 1];
+  int n;
+  if (refs_odo(env, f, pins, &n) || ref(env, out, &pins[5 * n])) return -1;
+  const uint8_t* ptrs[5 * MAXP];
+  size_t lens[5 * MAXP];
+  int64_t fail = -1;
+  pin_all(env, pins, 5 * n + 1);
+  ptrs_of(pins, 5 * n, ptrs, lens);
+  const int st = amphj_recombine_verify(CTX(ctx), n, ptrs, lens, (uint8_t*)pins[5 * n].p,
+                                        (size_t)pins[5 * n].len, &fail);
+  unpin_all(env, pins, 5 * n + 1, 5 * n);
+  if (st != AMPH_OK && st != AMPH_E_VERIFY) throw_status(env, st);
+  return st == AMPH_E_VERIFY ? (jlong)fail : -1;
+}
+
+/* createSecret arithmetic :150-160: verify the mask ODOs + maskInput per word */
+JNIEXPORT jlong JNICALL CLIENT(maskInput)(JNIEnv* env, jclass cls, jlong ctx, jobjectArray y, jobjectArray r,
+                                          jobjectArray v, jobjectArray w, jobjectArray u, jbyteArray secrets,
+                                          jbyteArray out) {
+  (void)cls;
+  jobjectArray f[5] = {y, r, v, w, u};
+  Pin pins[5 * MAXP + 2];
+  int n;
+  if (refs_odo(env, f, pins, &n) || ref(env, secrets, &pins[5 * n]) || ref(env, out, &pins[5 * n + 1])) return -1;
+  const uint8_t* ptrs[5 * MAXP];
+  size_t lens[5 * MAXP];
+  int64_t fail = -1;
+  pin_all(env, pins, 5 * n + 2);
+  ptrs_of(pins, 5 * n, ptrs, lens);
+  const int st = amphj_mask_input(CTX(ctx), n, ptrs, lens, (const uint8_t*)pins[5 * n].p, (size_t)pins[5 * n].len,
+                                  (uint8_t*)pins[5 * n + 1].p, (size_t)pins[5 * n + 1].len, &fail);
+  unpin_all(env, pins, 5 * n + 2, 5 * n + 1);
+  if (st != AMPH_OK && st != AMPH_E_VERIFY) throw_status(env, st);
+  return st == AMPH_E_VERIFY ? (jlong)fail : -1;
+}
+
+/* SecretShareUtil.recombineObject :70-90 */
+JNIEXPORT void JNICALL CLIENT(recombine)(JNIEnv* env, jclass cls, jlong ctx, jobjectArray shares, jbyteArray out) {
+  (void)cls;
+  Pin pins[MAXP + 1];
+  int n;
+  if (refs_list(env, shares, pins, &n) || ref(env, out, &pins[n])) return;
+  const uint8_t* ptrs[MAXP];
+  size_t lens[MAXP];
+  pin_all(env, pins, n + 1);
+  ptrs_of(pins, n, ptrs, lens);
+  const int st = amphj_recombine(CTX(ctx), n, ptrs, lens, (uint8_t*)pins[n].p, (size_t)pins[n].len);
+  unpin_all(env, pins, n + 1, n);
+  if (st != AMPH_OK) throw_status(env, st);
+}
+
+/* SecretShareUtil.verifySecrets :102-141 over canonical LE16 arrays -> -1 or the failing word */
+JNIEXPORT jlong JNICALL CLIENT(verify)(JNIEnv* env, jclass cls, jlong ctx, jbyteArray ys, jbyteArray rs,
+                                       jbyteArray us, jbyteArray vs, jbyteArray ws) {
+  (void)cls;
+  Pin pins[5];
+  jbyteArray a[5] = {ys, rs, us, vs, ws};
+  for (int k = 0; k < 5; ++k)
+    if (ref(env, a[k], &pins[k])) return -1;
+  const uint8_t* ptrs[5];
+  size_t lens[5];
+  int64_t fail = -1;
+  pin_all(env, pins, 5);
+  ptrs_of(pins, 5, ptrs, lens);
+  const int st = amphj_verify(CTX(ctx), ptrs, lens, &fail);
+  unpin_all(env, pins, 5, 5);
+  if (st != AMPH_OK && st != AMPH_E_VERIFY) throw_status(env, st);
+  return st == AMPH_E_VERIFY ? (jlong)fail : -1;
+}
+
+/* SecretShareUtil.maskInput :65-68 over canonical LE16 secrets and masks */
+JNIEXPORT void JNICALL CLIENT(maskWords)(JNIEnv* env, jclass cls, jlong ctx, jbyteArray secrets, jbyteArray masks,
+                                         jbyteArray out) {
+  (void)cls;
+  Pin pins[3];
+  if (ref(env, secrets, &pins[0]) || ref(env, masks, &pins[1]) || ref(env, out, &pins[2])) return;
+  pin_all(env, pins, 3);
+  const int st = amphj_mask_words(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len,
+                                  (const uint8_t*)pins[1].p, (size_t)pins[1].len, (uint8_t*)pins[2].p,
+                                  (size_t)pins[2].len);
+  unpin_all(env, pins, 3, 2);
+  if (st != AMPH_OK) throw_status(env, st);
+}
+
+/* the IntegrityVerificationException text of SecretShareUtil.java:116-129 */
+JNIEXPORT jstring JNICALL CLIENT(verifyMessage)(JNIEnv* env, jclass cls, jlong ctx, jbyteArray y, jbyteArray r,
+                                                jbyteArray u, jbyteArray v, jbyteArray w) {
+  (void)cls;
+  jbyteArray a[5] = {y, r, u, v, w};
+  jbyte b[5][16];
+  for (int k = 0; k < 5; ++k) {
+    if (!a[k] || (*env)->GetArrayLength(env, a[k]) != 16) return throw_arg(env, "16-byte words expected"), NULL;
+    (*env)->GetByteArrayRegion(env, a[k], 0, 16, b[k]);
+  }
+  char buf[1024];
+  const int st = amphj_verify_message(CTX(ctx), (const uint8_t*)b[0], (const uint8_t*)b[1], (const uint8_t*)b[2],
+                                      (const uint8_t*)b[3], (const uint8_t*)b[4], buf, sizeof buf);
+  if (st != AMPH_OK) {
+    throw_status(env, st);
+    return NULL;
+  }
+  return (*env)->NewStringUTF(env, buf);
+}
+
+/* getSecret straight from the five base64 strings per party (ASCII bytes) */
+JNIEXPORT jlong JNICALL CLIENT(recombineVerifyB64)(JNIEnv* env, jclass cls, jlong ctx, jobjectArray y,
+                                                   jobjectArray r, jobjectArray v, jobjectArray w, jobjectArray u,
+                                                   jlong words, jbyteArray out) {
+  (void)cls;
+  jobjectArray f[5] = {y, r, v, w, u};
+  Pin pins[5 * MAXP + 1];
+  int n;
+  if (words < 0) return throw_arg(env, "negative word count");
+  if (refs_odo(env, f, pins, &n) || ref(env, out, &pins[5 * n])) return -1;
+  const uint8_t* ptrs[5 * MAXP];
+  size_t lens[5 * MAXP];
+  int64_t fail = -1;
+  pin_all(env, pins, 5 * n + 1);
+  ptrs_of(pins, 5 * n, ptrs, lens);
+  const int st = amphj_recombine_verify_b64(CTX(ctx), n, (const char* const*)ptrs, lens, (size_t)words,
+                                            (uint8_t*)pins[5 * n].p, (size_t)pins[5 * n].len, &fail);
+  unpin_all(env, pins, 5 * n + 1, 5 * n);
+  if (st != AMPH_OK && st != AMPH_E_VERIFY) throw_status(env, st);
+  return st == AMPH_E_VERIFY ? (jlong)fail : -1;
+}
+
+/* createSecret from the /input-masks text: verify + mask + the 24-character MaskedInputData records */
+JNIEXPORT jlong JNICALL CLIENT(maskInputB64)(JNIEnv* env, jclass cls, jlong ctx, jobjectArray y, jobjectArray r,
+                                             jobjectArray v, jobjectArray w, jobjectArray u, jlong words,
+                                             jbyteArray secrets, jbyteArray records) {
+  (void)cls;
+  jobjectArray f[5] = {y, r, v, w, u};
+  Pin pins[5 * MAXP + 2];
+  int n;
+  if (words < 0) return throw_arg(env, "negative word count");
+  if (refs_odo(env, f, pins, &n) || ref(env, secrets, &pins[5 * n]) || ref(env, records, &pins[5 * n + 1]))
+    return -1;
+  const uint8_t* ptrs[5 * MAXP];
+  size_t lens[5 * MAXP];
+  int64_t fail = -1;
+  pin_all(env, pins, 5 * n + 2);
+  ptrs_of(pins, 5 * n, ptrs, lens);
+  const int st = amphj_mask_input_b64(CTX(ctx), n, (const char* const*)ptrs, lens, (size_t)words,
+                                      (const uint8_t*)pins[5 * n].p, (size_t)pins[5 * n].len,
+                                      (char*)pins[5 * n + 1].p, (size_t)pins[5 * n + 1].len, &fail);
+  unpin_all(env, pins, 5 * n + 2, 5 * n + 1);
+  if (st != AMPH_OK && st != AMPH_E_VERIFY) throw_status(env, st);
+  return st == AMPH_E_VERIFY ? (jlong)fail : -1;
+}
+
+/* ---- service ------------------------------------------------------------------ */
+#define SERVICE(name) Java_io_carbynestack_amphora_service_calculation_NativeShareArithmetic_##name
+
+JNIEXPORT jlong JNICALL SERVICE(ctxCreate)(JNIEnv* env, jclass cls, jbyteArray p, jbyteArray r,
+                                           jbyteArray rinv, jintArray devices) {
+  (void)cls;
+  return ctx_create(env, p, r, rinv, devices);
+}
+
+JNIEXPORT void JNICALL SERVICE(ctxDestroy)(JNIEnv* env, jclass cls, jlong ctx) {
+  (void)env;
+  (void)cls;
+  amphj_ctx_destroy(CTX(ctx));
+}
+
+/* SecretShareUtil.convertToSecretShare :58-107 -> SecretShare.data (32 B per word) */
+JNIEXPORT void JNICALL SERVICE(convertShare)(JNIEnv* env, jclass cls, jlong ctx, jbyteArray masked,
+                                             jbyteArray tuples, jbyteArray macKeyLe, jboolean useZeroInputAsData,
+                                             jbyteArray out) {
+  (void)cls;
+  Pin pins[4];
+  if (ref(env, masked, &pins[0]) || ref(env, tuples, &pins[1]) || ref(env, macKeyLe, &pins[2]) ||
+      ref(env, out, &pins[3]))
+    return;
+  pin_all(env, pins, 4);
+  const int st = amphj_convert_share(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len,
+                                     (const uint8_t*)pins[1].p, (size_t)pins[1].len, (const uint8_t*)pins[2].p,
+                                     (size_t)pins[2].len, useZeroInputAsData ? 1 : 0, (uint8_t*)pins[3].p,
+                                     (size_t)pins[3].len);
+  unpin_all(env, pins, 4, 3);
+  if (st != AMPH_OK) throw_status(env, st);
+}
+
+/* computeOutputDeliveryObject :100-139 + multiplyShares' local diffs :186-200 */
+JNIEXPORT void JNICALL SERVICE(odoPre)(JNIEnv* env, jclass cls, jlong ctx, jbyteArray share, jint stride,
+                                       jbyteArray masks, jbyteArray triples, jbyteArray y, jbyteArray r,
+                                       jbyteArray v, jbyteArray mag, jbyteArray neg) {
+  (void)cls;
+  Pin pins[8];
+  jbyteArray a[8] = {share, masks, triples, y, r, v, mag, neg};
+  for (int i = 0; i < 8; ++i)
+    if (ref(env, a[i], &pins[i])) return;
+  if (pins[3].len != pins[4].len || pins[3].len != pins[5].len) {
+    throw_arg(env, "The provided shares must be of the same length");
+    return;
+  }
+  pin_all(env, pins, 8);
+  const int st = amphj_odo_pre(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len, stride,
+                               (const uint8_t*)pins[1].p, (size_t)pins[1].len, (const uint8_t*)pins[2].p,
+                               (size_t)pins[2].len, (uint8_t*)pins[3].p, (uint8_t*)pins[4].p, (uint8_t*)pins[5].p,
+                               (size_t)pins[3].len, (uint8_t*)pins[6].p, (size_t)pins[6].len, (uint8_t*)pins[7].p,
+                               (size_t)pins[7].len);
+  unpin_all(env, pins, 8, 3);
+  if (st != AMPH_OK) throw_status(env, st);
+}
+
+/* recombineDiffs :231-272 + multiplySharedSecrets :274-286 + the w/u encoding :147-152 */
+JNIEXPORT void JNICALL SERVICE(openPost)(JNIEnv* env, jclass cls, jlong ctx, jobjectArray mags, jobjectArray negs,
+                                         jbyteArray triples, jboolean isPlayer0, jbyteArray w, jbyteArray u) {
+  (void)cls;
+  Pin pins[2 * MAXP + 3];
+  int n, n2;
+  if (refs_list(env, mags, pins, &n) || refs_list(env, negs, pins + n, &n2)) return;
+  if (n2 != n) {
+    throw_arg(env, "one sign array per magnitude array");
+    return;
+  }
+  if (ref(env, triples, &pins[2 * n]) || ref(env, w, &pins[2 * n + 1]) || ref(env, u, &pins[2 * n + 2])) return;
+  if (pins[2 * n + 1].len != pins[2 * n + 2].len) {
+    throw_arg(env, "The provided shares must be of the same length");
+    return;
+  }
+  const uint8_t* ptrs[2 * MAXP];
+  size_t lens[2 * MAXP];
+  pin_all(env, pins, 2 * n + 3);
+  ptrs_of(pins, 2 * n, ptrs, lens);
+  const int st = amphj_open_post(CTX(ctx), n, ptrs, lens, ptrs + n, lens + n, (const uint8_t*)pins[2 * n].p,
+                                 (size_t)pins[2 * n].len, isPlayer0 ? 1 : 0, (uint8_t*)pins[2 * n + 1].p,
+                                 (uint8_t*)pins[2 * n + 2].p, (size_t)pins[2 * n + 1].len);
+  unpin_all(env, pins, 2 * n + 3, 2 * n + 1);
+  if (st != AMPH_OK) throw_status(env, st);
+}
+
+/* MultiplicationExchangeObject.interimValues: signed diffs -> the JSON array text Jackson writes */
+JNIEXPORT jbyteArray JNICALL SERVICE(exchangeEncode)(JNIEnv* env, jclass cls, jlong ctx, jbyteArray mag,
+                                                     jbyteArray neg) {
+  (void)cls;
+  Pin pins[2];
+  if (ref(env, mag, &pins[0]) || ref(env, neg, &pins[1])) return NULL;
+  const size_t cap = amphj_exchange_max_chars((size_t)pins[0].len / 32);
+  char* text = (char*)malloc(cap ? cap : 1);
+  if (!text) {
+    jclass c = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+    if (c) (*env)->ThrowNew(env, c, "exchange text");
+    return NULL;
+  }
+  uint64_t len = 0;
+  pin_all(env, pins, 2);
+  const int st = amphj_exchange_encode(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len,
+                                       (const uint8_t*)pins[1].p, (size_t)pins[1].len, text, cap, &len);
+  unpin_all(env, pins, 2, 2);
+  jbyteArray out = NULL;
+  if (st != AMPH_OK) {
+    throw_status(env, st);
+  } else {
+    out = (*env)->NewByteArray(env, (jsize)len);
+    if (out) (*env)->SetByteArrayRegion(env, out, 0, (jsize)len, (const jbyte*)text);
+  }
+  free(text);
+  return out;
+}
+
+/* the interimValues array span of a received body -> signed diffs */
+JNIEXPORT void JNICALL SERVICE(exchangeDecode)(JNIEnv* env, jclass cls, jlong ctx, jbyteArray body, jint off,
+                                               jint len, jlong npairs, jbyteArray mag, jbyteArray neg) {
+  (void)cls;
+  Pin pins[3];
+  if (ref(env, body, &pins[0]) || ref(env, mag, &pins[1]) || ref(env, neg, &pins[2])) return;
+  if (off < 0 || len < 0 || (jlong)off + len > pins[0].len || npairs < 0) {
+    throw_arg(env, "interimValues span outside the body");
+    return;
+  }
+  pin_all(env, pins, 3);
+  const int st = amphj_exchange_decode(CTX(ctx), (const char*)pins[0].p + off, (size_t)len, (size_t)npairs,
+                                       (uint8_t*)pins[1].p, (size_t)pins[1].len, (uint8_t*)pins[2].p,
+                                       (size_t)pins[2].len);
+  unpin_all(env, pins, 3, 1);
+  if (st != AMPH_OK) throw_status(env, st);
+}

@@ -1,0 +1,178 @@
+/*
+ * TEST HARNESS ONLY: a mock JNIEnv over plain C arrays (see jni.h here).
+ * Built with jni/amphora_jni.c and jni/amphora_jni_core.c into
+ * libjni_mock.so, which tests/test_jni_core.py drives through ctypes: Java
+ * arrays are made with mock_bytes / mock_objects, the Java_* entry points are
+ * called with mock_env(), and the mock records the thrown exception, the
+ * release mode of every pinned array, and any JNI call made inside a
+ * critical region (a JNI rule the layer must keep).
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "jni.h"
+
+enum { KIND_BYTES = 1, KIND_INTS, KIND_OBJECTS, KIND_CLASS, KIND_STRING };
+
+struct mock_obj {
+  int kind;
+  jsize len;
+  void* data;          /* bytes / ints / jobject* / char* */
+  int pinned;          /* open critical pins of this array */
+  int released_commit; /* releases with mode 0 (copy back) */
+  int released_abort;  /* releases with JNI_ABORT */
+  struct mock_obj* next;
+};
+
+static struct mock_obj* g_all;
+static int g_critical;    /* open critical regions */
+static int g_violations;  /* JNI calls made inside one */
+static char g_exc_class[256];
+static char g_exc_msg[1024];
+
+static struct mock_obj* obj_new(int kind, jsize len, size_t elem) {
+  struct mock_obj* o = (struct mock_obj*)calloc(1, sizeof *o);
+  o->kind = kind;
+  o->len = len;
+  o->data = calloc(len > 0 ? (size_t)len : 1, elem);
+  o->next = g_all;
+  g_all = o;
+  return o;
+}
+
+static void outside_critical(void) {
+  if (g_critical) ++g_violations;
+}
+
+static jclass m_FindClass(JNIEnv* env, const char* name) {
+  (void)env;
+  outside_critical();
+  struct mock_obj* o = obj_new(KIND_CLASS, (jsize)strlen(name) + 1, 1);
+  memcpy(o->data, name, strlen(name) + 1);
+  return o;
+}
+
+static jint m_ThrowNew(JNIEnv* env, jclass c, const char* msg) {
+  (void)env;
+  outside_critical();
+  if (!g_exc_class[0]) {  /* the first pending exception wins, as in a JVM */
+    strncpy(g_exc_class, (const char*)c->data, sizeof g_exc_class - 1);
+    strncpy(g_exc_msg, msg ? msg : "", sizeof g_exc_msg - 1);
+  }
+  return 0;
+}
+
+static jsize m_GetArrayLength(JNIEnv* env, jarray a) {
+  (void)env;
+  outside_critical();
+  return a->len;
+}
+
+static jobject m_GetObjectArrayElement(JNIEnv* env, jobjectArray a, jsize i) {
+  (void)env;
+  outside_critical();
+  return (i >= 0 && i < a->len) ? ((jobject*)a->data)[i] : NULL;
+}
+
+static void* m_GetPrimitiveArrayCritical(JNIEnv* env, jarray a, jboolean* is_copy) {
+  (void)env;
+  if (is_copy) *is_copy = JNI_FALSE;
+  ++g_critical;
+  ++a->pinned;
+  return a->data;
+}
+
+static void m_ReleasePrimitiveArrayCritical(JNIEnv* env, jarray a, void* p, jint mode) {
+  (void)env;
+  (void)p;
+  --g_critical;
+  --a->pinned;
+  if (mode == JNI_ABORT) ++a->released_abort;
+  else ++a->released_commit;
+}
+
+static void m_GetIntArrayRegion(JNIEnv* env, jintArray a, jsize start, jsize len, jint* buf) {
+  (void)env;
+  outside_critical();
+  memcpy(buf, (jint*)a->data + start, (size_t)len * sizeof(jint));
+}
+
+static void m_GetByteArrayRegion(JNIEnv* env, jbyteArray a, jsize start, jsize len, jbyte* buf) {
+  (void)env;
+  outside_critical();
+  memcpy(buf, (jbyte*)a->data + start, (size_t)len);
+}
+
+static void m_SetByteArrayRegion(JNIEnv* env, jbyteArray a, jsize start, jsize len, const jbyte* buf) {
+  (void)env;
+  outside_critical();
+  memcpy((jbyte*)a->data + start, buf, (size_t)len);
+}
+
+static jbyteArray m_NewByteArray(JNIEnv* env, jsize len) {
+  (void)env;
+  outside_critical();
+  return obj_new(KIND_BYTES, len, 1);
+}
+
+static jstring m_NewStringUTF(JNIEnv* env, const char* s) {
+  (void)env;
+  outside_critical();
+  struct mock_obj* o = obj_new(KIND_STRING, (jsize)strlen(s), 1);
+  free(o->data);
+  o->data = strdup(s);
+  return o;
+}
+
+static const struct JNINativeInterface_ g_table = {
+    m_FindClass,          m_ThrowNew,          m_GetArrayLength,     m_GetObjectArrayElement,
+    m_GetPrimitiveArrayCritical, m_ReleasePrimitiveArrayCritical, m_GetIntArrayRegion,
+    m_GetByteArrayRegion, m_SetByteArrayRegion, m_NewByteArray,      m_NewStringUTF,
+};
+static JNIEnv g_env = &g_table;
+
+/* ---- harness API (ctypes) ---- */
+JNIEXPORT JNIEnv* mock_env(void) { return &g_env; }
+
+JNIEXPORT jobject mock_bytes(const uint8_t* data, jsize len) {
+  struct mock_obj* o = obj_new(KIND_BYTES, len, 1);
+  if (data && len) memcpy(o->data, data, (size_t)len);
+  return o;
+}
+
+JNIEXPORT jobject mock_ints(const int32_t* data, jsize len) {
+  struct mock_obj* o = obj_new(KIND_INTS, len, sizeof(jint));
+  if (data && len) memcpy(o->data, data, (size_t)len * sizeof(jint));
+  return o;
+}
+
+JNIEXPORT jobject mock_objects(jobject* elems, jsize len) {
+  struct mock_obj* o = obj_new(KIND_OBJECTS, len, sizeof(jobject));
+  memcpy(o->data, elems, (size_t)len * sizeof(jobject));
+  return o;
+}
+
+JNIEXPORT jsize mock_len(jobject o) { return o ? o->len : -1; }
+JNIEXPORT const void* mock_data(jobject o) { return o ? o->data : NULL; }
+JNIEXPORT int mock_commits(jobject o) { return o->released_commit; }
+JNIEXPORT int mock_aborts(jobject o) { return o->released_abort; }
+JNIEXPORT const char* mock_exception_class(void) { return g_exc_class; }
+JNIEXPORT const char* mock_exception_message(void) { return g_exc_msg; }
+JNIEXPORT int mock_violations(void) { return g_violations; }
+JNIEXPORT int mock_open_criticals(void) { return g_critical; }
+
+JNIEXPORT void mock_clear(void) {
+  g_exc_class[0] = g_exc_msg[0] = 0;
+  g_violations = 0;
+}
+
+JNIEXPORT void mock_free_all(void) {
+  while (g_all) {
+    struct mock_obj* n = g_all->next;
+    free(g_all->data);
+    free(g_all);
+    g_all = n;
+  }
+  g_critical = 0;
+  mock_clear();
+}

@@ -1,0 +1,289 @@
+"""The JNI layer (jni/amphora_jni.c + jni/amphora_jni_core.c) driven through a
+mock JNIEnv (tests/jni_mock/, test harness only -- no JDK exists here).
+
+CPU: the status -> Java exception mapping; argument and length checks that
+must fire before anything reaches the C ABI (a Java byte[] shorter than the
+word count implies would otherwise be read or written past its end); the
+JNI rules -- no JNI call inside a critical region, every pinned array
+released, inputs released with JNI_ABORT and outputs committed.
+GPU: every Java entry point against the C oracle / the ABI through Python on
+the same inputs -- the client's recombineVerify / maskInput / verify /
+recombine / maskWords / verifyMessage / the base64 variants, the service's
+convertShare / odoPre / exchange encode+decode / openPost (a 2-party Output
+Delivery run entirely through the JNI entry points).
+"""
+import base64
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import amphora_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MOCK = os.path.join(ROOT, "tests", "jni_mock", "libjni_mock.so")
+P, R, RINV = O.TEST_PRIME, O.TEST_R, O.TEST_RINV
+CLIENT = "Java_io_carbynestack_amphora_client_NativeShareArithmetic_"
+SERVICE = "Java_io_carbynestack_amphora_service_calculation_NativeShareArithmetic_"
+IAE = "java/lang/IllegalArgumentException"
+
+
+@pytest.fixture(scope="module")
+def J():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "jni"), "mock"], check=True)
+    L = C.CDLL(MOCK)
+    vp = C.c_void_p
+    L.mock_env.restype = vp
+    for f in ("mock_bytes", "mock_ints", "mock_objects"):
+        getattr(L, f).restype = vp
+    L.mock_bytes.argtypes = [C.c_char_p, C.c_int32]
+    L.mock_ints.argtypes = [C.POINTER(C.c_int32), C.c_int32]
+    L.mock_objects.argtypes = [C.POINTER(vp), C.c_int32]
+    L.mock_len.argtypes = [vp]
+    L.mock_data.restype = vp
+    L.mock_data.argtypes = [vp]
+    L.mock_commits.argtypes = L.mock_aborts.argtypes = [vp]
+    L.mock_exception_class.restype = L.mock_exception_message.restype = C.c_char_p
+    L.amphj_exception_class.restype = C.c_char_p
+    return L
+
+
+class Env:
+    """Java-side helpers over the mock: arrays in, results out."""
+
+    def __init__(self, L):
+        self.L = L
+        self.env = L.mock_env()
+        L.mock_free_all()
+
+    def bytes(self, b):
+        b = bytes(np.ascontiguousarray(b).tobytes()) if isinstance(b, np.ndarray) else bytes(b)
+        return self.L.mock_bytes(b, len(b))
+
+    def zeros(self, n):
+        return self.L.mock_bytes(None, n)
+
+    def objects(self, objs):
+        arr = (C.c_void_p * len(objs))(*objs)
+        return self.L.mock_objects(arr, len(objs))
+
+    def read(self, obj):
+        n = self.L.mock_len(obj)
+        return C.string_at(self.L.mock_data(obj), n) if n > 0 else b""
+
+    def call(self, name, restype, *args):
+        fn = getattr(self.L, name)
+        fn.restype = restype
+        conv = [C.c_void_p(self.env), C.c_void_p(None)]
+        for a in args:
+            conv.append(a if isinstance(a, C._SimpleCData) else C.c_void_p(a))
+        return fn(*conv)
+
+    def exception(self):
+        cls = self.L.mock_exception_class().decode()
+        return (cls, self.L.mock_exception_message().decode()) if cls else None
+
+    def clean(self):
+        """JNI rules held: nothing called inside a critical region, nothing left pinned."""
+        return self.L.mock_violations() == 0 and self.L.mock_open_criticals() == 0
+
+    def odo_lists(self, odos):
+        return [self.objects([self.bytes(o[k]) for o in odos]) for k in range(5)]
+
+
+def le16(x):
+    return int(x).to_bytes(16, "little")
+
+
+def test_exception_mapping(J):
+    assert J.amphj_exception_class(0) is None
+    assert J.amphj_exception_class(1) == b"io/carbynestack/amphora/common/exceptions/IntegrityVerificationException"
+    assert J.amphj_exception_class(2) == J.amphj_exception_class(3) == IAE.encode()
+    assert J.amphj_exception_class(4) == J.amphj_exception_class(5) == b"java/lang/IllegalStateException"
+
+
+def test_checks_fire_before_the_abi(J):
+    """No context is needed: each case is rejected before libamphora_hip is called."""
+    e = Env(J)
+    ctx = C.c_int64(0)
+    word = e.bytes(b"\0" * 32)
+    short = e.bytes(b"\0" * 16)
+    # parties out of range
+    empty = e.objects([])
+    assert e.call(CLIENT + "recombineVerify", C.c_int64, ctx, empty, empty, empty, empty, empty, e.zeros(32)) == -1
+    assert e.exception() == (IAE, "n_parties must be in [1, 16]") and e.clean()
+    # one field shorter than the others (ADVICE r2's over-read, at the JNI boundary)
+    J.mock_clear()
+    lists = [e.objects([word, word]) for _ in range(4)] + [e.objects([word, short])]
+    assert e.call(CLIENT + "recombineVerify", C.c_int64, ctx, *lists, e.zeros(32)) == -1
+    assert e.exception() == (IAE, "The provided shares must be of the same length") and e.clean()
+    # output array too short for the words
+    J.mock_clear()
+    lists = [e.objects([word, word]) for _ in range(5)]
+    out = e.zeros(16)
+    e.call(CLIENT + "recombineVerify", C.c_int64, ctx, *lists, out)
+    cls, msg = e.exception()
+    assert cls == IAE and "secrets array holds 16 bytes, 32 needed" in msg and e.clean()
+    assert J.mock_aborts(word) >= 1 and J.mock_commits(word) == 0  # inputs never copied back
+    assert J.mock_commits(out) == 1
+    # service: SecretShareUtil.java:64-66
+    J.mock_clear()
+    e.call(SERVICE + "convertShare", None, ctx, e.bytes(b"\0" * 32), e.bytes(b"\0" * 32), e.bytes(b"\0" * 16),
+           C.c_uint8(0), e.zeros(64))
+    assert e.exception() == (IAE, "Received more input data than available inputMasks.") and e.clean()
+    # odoPre: the triple stream must hold 2W triples
+    J.mock_clear()
+    e.call(SERVICE + "odoPre", None, ctx, e.bytes(b"\0" * 64), C.c_int32(32), e.bytes(b"\0" * 128),
+           e.bytes(b"\0" * 100), e.zeros(32), e.zeros(32), e.zeros(32), e.zeros(128), e.zeros(8))
+    cls, msg = e.exception()
+    assert cls == IAE and "triple stream" in msg and e.clean()
+    # exchange decode span outside the body
+    J.mock_clear()
+    e.call(SERVICE + "exchangeDecode", None, ctx, e.bytes(b"[]"), C.c_int32(1), C.c_int32(5), C.c_int64(0),
+           e.zeros(0), e.zeros(0))
+    assert e.exception() == (IAE, "interimValues span outside the body") and e.clean()
+    # context parameters must be 16-byte integers
+    J.mock_clear()
+    assert e.call(CLIENT + "ctxCreate", C.c_int64, e.bytes(b"\1" * 8), e.bytes(b"\0" * 16), e.bytes(b"\0" * 16),
+                  None) == 0
+    assert e.exception()[0] == IAE and e.clean()
+
+
+# ---------------------------------------------------------------- GPU --------
+@pytest.fixture(scope="module")
+def jctx(J):
+    import torch
+    assert torch.cuda.is_available()
+    e = Env(J)
+    h = e.call(CLIENT + "ctxCreate", C.c_int64, e.bytes(le16(P)), e.bytes(le16(R)), e.bytes(le16(RINV)), None)
+    assert h != 0 and e.exception() is None
+    yield h
+    Env(J).call(CLIENT + "ctxDestroy", None, C.c_int64(h))
+
+
+@pytest.fixture(scope="module")
+def F():
+    from oracle import coracle
+    return coracle.test_field(threads=8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,W", [(2, 1000), (3, 5000), (2, 70_000)])
+def test_client_entry_points(J, jctx, F, n, W):
+    e = Env(J)
+    ctx = C.c_int64(jctx)
+    odos, _ = F.synth_odos(seed=W + n, n=n, W=W, noncanon_permille=10)
+    oy, off = F.recombine_verify(odos)
+    out = e.zeros(16 * W)
+    assert e.call(CLIENT + "recombineVerify", C.c_int64, ctx, *e.odo_lists(odos), out) == -1
+    assert e.exception() is None and e.clean() and e.read(out) == oy.tobytes()
+    bad, _ = F.synth_odos(seed=W + n, n=n, W=W, fault_index=W // 3)
+    assert e.call(CLIENT + "recombineVerify", C.c_int64, ctx, *e.odo_lists(bad), e.zeros(16 * W)) == W // 3
+    assert e.exception() is None  # a verify failure is returned, the Java side renders the message
+    secrets = F.synth_words(seed=7, count=W - 3, mont=False)
+    om, _ = F.mask_input(secrets, [tuple(f[: W - 3] for f in o) for o in odos])
+    out = e.zeros(16 * (W - 3))
+    assert e.call(CLIENT + "maskInput", C.c_int64, ctx, *e.odo_lists(odos), e.bytes(secrets), out) == -1
+    assert e.read(out) == om.tobytes() and e.clean()
+    # recombine / verify / maskWords on the recombined fields
+    f = [F.recombine([o[k] for o in odos]) for k in range(5)]  # y, r, v, w, u canonical
+    out = e.zeros(16 * W)
+    e.call(CLIENT + "recombine", None, ctx, e.objects([e.bytes(o[0]) for o in odos]), out)
+    assert e.read(out) == f[0].tobytes()
+    assert e.call(CLIENT + "verify", C.c_int64, ctx, *[e.bytes(f[k]) for k in (0, 1, 4, 2, 3)]) == -1
+    f3 = f[3].copy()
+    f3[W // 2, 0] ^= 1
+    assert e.call(CLIENT + "verify", C.c_int64, ctx, e.bytes(f[0]), e.bytes(f[1]), e.bytes(f[4]), e.bytes(f[2]),
+                  e.bytes(f3)) == W // 2
+    masks = F.synth_words(seed=8, count=W, mont=False)
+    out = e.zeros(16 * W)
+    e.call(CLIENT + "maskWords", None, ctx, e.bytes(secrets[:W // 2]), e.bytes(masks[:W // 2]), out)
+    exp = b"".join(((((int.from_bytes(s.tobytes(), "little") - int.from_bytes(m.tobytes(), "little")) % P) * R % P)
+                    .to_bytes(16, "little")) for s, m in zip(secrets[:W // 2], masks[:W // 2]))
+    assert e.read(out)[: len(exp)] == exp and e.clean()
+
+
+@pytest.mark.gpu
+def test_client_text_entry_points_and_message(J, jctx, F):
+    import amphora_amd as A
+    e = Env(J)
+    ctx = C.c_int64(jctx)
+    W, n = 3000, 2
+    odos, _ = F.synth_odos(seed=5, n=n, W=W)
+    texts = [[base64.b64encode(np.ascontiguousarray(f).tobytes()) for f in o] for o in odos]
+    tl = [e.objects([e.bytes(t[k]) for t in texts]) for k in range(5)]
+    out = e.zeros(16 * W)
+    assert e.call(CLIENT + "recombineVerifyB64", C.c_int64, ctx, *tl, C.c_int64(W), out) == -1
+    assert e.read(out) == F.recombine_verify(odos)[0].tobytes() and e.clean()
+    secrets = F.synth_words(seed=6, count=W, mont=False)
+    rec = e.zeros(24 * W)
+    assert e.call(CLIENT + "maskInputB64", C.c_int64, ctx, *tl, C.c_int64(W), e.bytes(secrets), rec) == -1
+    om, _ = F.mask_input(secrets, odos)
+    assert e.read(rec) == b"".join(base64.b64encode(w.tobytes()) for w in om)
+    # a bad character: IllegalArgumentException naming party, field, offset
+    t2 = bytearray(texts[1][2])
+    t2[77] = ord("*")
+    tl[2] = e.objects([e.bytes(texts[0][2]), e.bytes(bytes(t2))])
+    J.mock_clear()
+    e.call(CLIENT + "recombineVerifyB64", C.c_int64, ctx, *tl, C.c_int64(W), e.zeros(16 * W))
+    cls, msg = e.exception()
+    assert cls == IAE and "index 77 of party 1's vShares" in msg and e.clean()
+    # the reference's failure text (SecretShareUtil.java:116-129)
+    ref = A.Context(P, R, RINV)
+    vals = [12345, 678, 91011, 1213, 1415]
+    s = e.call(CLIENT + "verifyMessage", C.c_void_p, ctx, *[e.bytes(le16(x)) for x in vals])
+    assert e.read(s).decode() == ref.verify_message(*vals)
+
+
+@pytest.mark.gpu
+def test_service_entry_points_two_party_output_delivery(J, jctx, F):
+    """convertShare (KAT-free, against the oracle) and a full 2-party Output
+    Delivery through odoPre -> exchangeEncode -> exchangeDecode -> openPost."""
+    e = Env(J)
+    ctx = C.c_int64(jctx)
+    W = 777
+    masked = F.synth_words(seed=11, count=W)
+    tuples = F.synth_words(seed=12, count=2 * W).reshape(W, 32)
+    key = 0x1234567890ABCDEF1234567890ABCD % P
+    for use_zero in (0, 1):
+        out = e.zeros(32 * W)
+        e.call(SERVICE + "convertShare", None, ctx, e.bytes(masked), e.bytes(tuples), e.bytes(le16(key)),
+               C.c_uint8(use_zero), out)
+        assert e.exception() is None and e.clean()
+        assert e.read(out) == F.convert_share(masked, tuples, key, bool(use_zero)).tobytes()
+    # Output Delivery: each party's share data (stride 32), masks (2W x 32 B), triples (2W x 96 B)
+    shares = [F.synth_words(seed=20 + j, count=2 * W).reshape(W, 32) for j in range(2)]
+    masks = [F.synth_words(seed=30 + j, count=4 * W).reshape(2 * W, 32) for j in range(2)]
+    triples = [F.synth_words(seed=40 + j, count=12 * W).reshape(2 * W, 96) for j in range(2)]
+    pre, texts = [], []
+    for j in range(2):
+        y, r, v, mag, neg = (e.zeros(16 * W), e.zeros(16 * W), e.zeros(16 * W), e.zeros(64 * W), e.zeros(4 * W))
+        e.call(SERVICE + "odoPre", None, ctx, e.bytes(shares[j]), C.c_int32(32), e.bytes(masks[j]),
+               e.bytes(triples[j]), y, r, v, mag, neg)
+        assert e.exception() is None and e.clean()
+        oy, orr, ov, omag, oneg = F.odo_pre(shares[j], 32, masks[j], triples[j])
+        assert [e.read(x) for x in (y, r, v, mag, neg)] == [a.tobytes() for a in (oy, orr, ov, omag, oneg)]
+        txt = e.call(SERVICE + "exchangeEncode", C.c_void_p, ctx, mag, neg)
+        assert e.exception() is None and e.read(txt).startswith(b'[{"a":')
+        pre.append((omag, oneg))
+        texts.append(e.read(txt))
+    for j in range(2):
+        mags, negs = [], []
+        for k in (j, 1 - j):  # own diffs first, then the partner's decoded from its text
+            body = b'{"interimValues":' + texts[k] + b"}"
+            mag, neg = e.zeros(64 * W), e.zeros(4 * W)
+            e.call(SERVICE + "exchangeDecode", None, ctx, e.bytes(body), C.c_int32(17), C.c_int32(len(texts[k])),
+                   C.c_int64(2 * W), mag, neg)
+            assert e.exception() is None and e.clean()
+            assert e.read(mag) == pre[k][0].tobytes() and e.read(neg) == pre[k][1].tobytes()
+            mags.append(mag)
+            negs.append(neg)
+        w, u = e.zeros(16 * W), e.zeros(16 * W)
+        e.call(SERVICE + "openPost", None, ctx, e.objects(mags), e.objects(negs), e.bytes(triples[j]),
+               C.c_uint8(j == 0), w, u)
+        assert e.exception() is None and e.clean()
+        opened = F.recombine_diffs([pre[j][0], pre[1 - j][0]], [pre[j][1], pre[1 - j][1]])
+        ow, ou = F.odo_post(opened, triples[j], j == 0)
+        assert e.read(w) == ow.tobytes() and e.read(u) == ou.tobytes()

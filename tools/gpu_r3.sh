@@ -20,7 +20,7 @@ step() {  # step NAME SECONDS CMD...
 }
 run_all() {
   [ -n "$SKIP_SMOKE" ] || step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" || return
-  [ -n "$SKIP_TESTS" ] || step pytest 1500 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} || return
+  [ -n "$SKIP_TESTS" ] || step pytest 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} || return
   step bench_c2 300 python3 bench.py || return
   step bench_c4_n1 300 python3 bench.py --workload c4 --no-cpu-baseline || return
   step bench_c4_gloo2 300 python3 bench.py --gpus 2 --backend gloo --same-device || return
