@@ -1,0 +1,27 @@
+#!/bin/bash
+# CPU side: exchange-decode variants for an A/B on the GPU (tools/gpu_xdec.sh).
+# Each variant is exchange.hip with one sed edit, compiled into the
+# ubench_xdec2 harness (tools/ubench/ubench_xdec2.hip includes XDEC_SRC).
+# Output: tools/ubench/xv/ (git-ignored; travels to the GPU box).
+set -e
+ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+X="$ROOT/amphora_amd/csrc/exchange.hip"
+D="$ROOT/tools/ubench/xv"
+mkdir -p "$D"
+variant() {  # name sed-expression...
+  local name=$1
+  shift
+  cp "$X" "$D/exchange_$name.hip"
+  for e in "$@"; do sed -i "$e" "$D/exchange_$name.hip"; done
+  cmp -s "$X" "$D/exchange_$name.hip" && [ "$name" != base ] && { echo "variant $name: sed changed nothing" >&2; exit 1; }
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I"$ROOT/include" -I"$ROOT/amphora_amd/csrc" \
+    -DXDEC_SRC="\"$D/exchange_$name.hip\"" "$ROOT/tools/ubench/ubench_xdec2.hip" -o "$D/ubench_xdec2_$name" &
+}
+variant base
+# the compact pass without its parse loop (window + colon listing + scan only)
+variant noparse 's/for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {/for (uint32_t idx = threadIdx.x; idx < 0u; idx += kDecBlock) {/'
+# digit run + segment checks, no base-10^8 conversion
+variant noconv 's/^  const uint32_t full = nd >> 3, rem = nd \& 7u;$/  r.v[0] = nd; r.v[1] = r.v[2] = r.v[3] = 0; return true;\n  const uint32_t full = nd >> 3, rem = nd \& 7u;/'
+for v in "$@"; do :; done
+wait
+ls -la "$D"
