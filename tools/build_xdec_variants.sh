@@ -8,16 +8,18 @@ ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 X="$ROOT/amphora_amd/csrc/exchange.hip"
 D="$ROOT/tools/ubench/xv"
 mkdir -p "$D"
-variant() {  # name sed-expression...
-  local name=$1
+variant() {  # name [-Dflags] sed-expression...
+  local name=$1 defs=""
   shift
+  while [ "${1#-D}" != "$1" ]; do defs="$defs $1"; shift; done
   cp "$X" "$D/exchange_$name.hip"
   for e in "$@"; do sed -i "$e" "$D/exchange_$name.hip"; done
-  cmp -s "$X" "$D/exchange_$name.hip" && [ "$name" != base ] && { echo "variant $name: sed changed nothing" >&2; exit 1; }
+  cmp -s "$X" "$D/exchange_$name.hip" && [ "$name" != base ] && [ -z "$defs" ] && { echo "variant $name: sed changed nothing" >&2; exit 1; }
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I"$ROOT/include" -I"$ROOT/amphora_amd/csrc" \
-    -DXDEC_SRC="\"$D/exchange_$name.hip\"" "$ROOT/tools/ubench/ubench_xdec2.hip" -o "$D/ubench_xdec2_$name" &
+    $defs -DXDEC_SRC="\"$D/exchange_$name.hip\"" "$ROOT/tools/ubench/ubench_xdec2.hip" -o "$D/ubench_xdec2_$name" &
 }
 variant base
+# count pass with plain loads (text tail left in the Infinity Cache), compact pass from the end
 # the compact pass without its parse loop (window + colon listing + scan only)
 variant noparse 's/for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {/for (uint32_t idx = threadIdx.x; idx < 0u; idx += kDecBlock) {/'
 # digit run + segment checks, no base-10^8 conversion

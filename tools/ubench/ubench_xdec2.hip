@@ -49,6 +49,28 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(&L, len, 8, hipMemcpyDeviceToHost));
   CK(hipMalloc(&s2, xdec_scratch_bytes(L)));
   printf("text %llu bytes for %zu pairs\n", L, npairs);
+  {  // the encode that made it, timed the same way (text compared with the first run's)
+    hipEvent_t f0, f1;
+    CK(hipEventCreate(&f0)); CK(hipEventCreate(&f1));
+    std::vector<char> ref(L), got(L);
+    CK(hipMemcpy(ref.data(), text, L, hipMemcpyDeviceToHost));
+    std::vector<float> te;
+    for (int r = 0; r < R + 3; ++r) {
+      CK(hipEventRecord(f0, 0));
+      CK(launch_exchange_encode(mag, neg, npairs, text, len, s1, c));
+      CK(hipEventRecord(f1, 0));
+      CK(hipEventSynchronize(f1));
+      float ms; CK(hipEventElapsedTime(&ms, f0, f1));
+      if (r >= 3) te.push_back(ms);
+    }
+    unsigned long long L2;
+    CK(hipMemcpy(&L2, len, 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(got.data(), text, L, hipMemcpyDeviceToHost));
+    std::sort(te.begin(), te.end());
+    printf("encode %s, median %8.1f us  min %8.1f us  %6.2f TB/s of text\n",
+           L2 == L && got == ref ? "text identical" : "TEXT DIFFERS", te[te.size() / 2] * 1e3, te[0] * 1e3,
+           L / (te[te.size() / 2] * 1e-3) / 1e12);
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   std::vector<float> ts;
