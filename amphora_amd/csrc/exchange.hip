@@ -259,15 +259,19 @@ struct Hier {
 };
 constexpr int kGroupSpans = 64;  // units per l1 group = per counting workgroup
 
+// Counts live in bits 0..39 of the words; the decode's single pass marks
+// each publication in bits 40..63 (kOne per contributor, see k_xdec_one).
+constexpr uint64_t kOne = 1ull << 40, kCountMask = kOne - 1;
+
 // call with a whole wave; every lane returns the prefix
 __device__ __forceinline__ uint64_t hier_prefix(const Hier& h, size_t s) {
   const size_t lane = __lane_id();
   uint64_t v = 0;
-  for (size_t k = lane; k < (s >> 12); k += 64) v += h.l2[k];
+  for (size_t k = lane; k < (s >> 12); k += 64) v += h.l2[k] & kCountMask;
   const size_t g0 = (s >> 12) << 6, g1 = s >> 6;
-  if (g0 + lane < g1) v += h.l1[g0 + lane];
+  if (g0 + lane < g1) v += h.l1[g0 + lane] & kCountMask;
   const size_t s0 = (s >> 6) << 6;
-  if (s0 + lane < s) v += h.l0[s0 + lane];
+  if (s0 + lane < s) v += h.l0[s0 + lane] & kCountMask;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
@@ -276,15 +280,15 @@ __device__ __forceinline__ uint64_t hier_prefix(const Hier& h, size_t s) {
 // every unit's count: one wave
 __device__ __forceinline__ uint64_t hier_total(const Hier& h, size_t n) {
   uint64_t v = 0;
-  for (size_t k = __lane_id(); k < ((n + 4095) >> 12); k += 64) v += h.l2[k];
+  for (size_t k = __lane_id(); k < ((n + 4095) >> 12); k += 64) v += h.l2[k] & kCountMask;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 
-__global__ __launch_bounds__(256) void k_hier_zero(uint64_t* l2, size_t n2, unsigned int* flags, int nflags) {
-  for (size_t i = threadIdx.x; i < n2; i += 256) l2[i] = 0;
-  if ((int)threadIdx.x < nflags) flags[threadIdx.x] = 0;
+__global__ __launch_bounds__(256) void k_hier_zero(uint64_t* w, size_t n, unsigned int* flags, int nflags) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) w[i] = 0;
+  if (blockIdx.x == 0 && (int)threadIdx.x < nflags) flags[threadIdx.x] = 0;
 }
 
 // Encode pass 1: the text length of each 256-pair block's run of entries
@@ -468,86 +472,11 @@ constexpr size_t kDecSpan = (size_t)kDecBlock * kDecBytes;  // 8 KiB of text per
 constexpr int kWinPad = 256;                           // window context either side
 constexpr int kWin = (int)kDecSpan + 2 * kWinPad;      // staged bytes
 
-// Flags of one decode, zeroed with the l2 words before the count pass (k_hier_zero):
-// [0] some span wholly inside the text holds whitespace or a control byte (the
-// compact pass cannot hold: the general pass does it all), [1] k_xdec_fast met
-// a value outside the compact layout.
-
-// Pass 1: colons (= numbers) per 8 KiB span.  One workgroup per 64-span group,
-// each wave 16 consecutive spans in turn: per span 64 lanes x eight 16-B
-// loads, lane-interleaved so that every wave instruction reads 1 KiB
-// contiguous (nontemporal: the text is read once here and once by the parse),
-// a wave reduction, no LDS or barrier; then the group sum to l1 (a plain
-// store) and l2 (one atomic add per group).  96 us per 640 MB text where 128
-// lanes x 64 lane-contiguous bytes per span took 162
-// (tools/ubench/ubench_xcount.hip).
-constexpr int kCntWaves = 4;
-// Cache policy of the count pass's text loads and the compact pass's span
-// order (A/B knobs): with plain loads the count pass leaves the last ~256 MiB
-// of the text in the Infinity Cache, and a compact pass that walks the spans
-// from the end reads that part from it instead of HBM.  Measured: plain loads
-// cost the count pass 17 % and the compact pass gains less (r03 xdec2 A/B).
-#ifndef AMPH_XDEC_COUNT_NT
-#define AMPH_XDEC_COUNT_NT 1
-#endif
-#ifndef AMPH_XDEC_REVERSE
-#define AMPH_XDEC_REVERSE 0
-#endif
-
-__device__ __forceinline__ uint32_t swar_below21(uint32_t w) {  // nonzero iff some byte < 0x21
-  return (w - 0x21212121u) & ~w & 0x80808080u;
-}
-
-__global__ __launch_bounds__(64 * kCntWaves) void k_xdec_count(Text t, Hier h, size_t nb,
-                                                             unsigned int* flags) {
-  constexpr int kPerWave = kGroupSpans / kCntWaves;
-  const size_t group = blockIdx.x;
-  const int wave = threadIdx.x >> 6;
-  uint32_t gsum = 0;
-  bool ws_any = false;
-  for (int j = 0; j < kPerWave; ++j) {
-    const size_t span = group * kGroupSpans + (size_t)wave * kPerWave + j;
-    if (span >= nb) break;
-    const size_t base = span * kDecSpan + (size_t)(threadIdx.x & 63) * 16;
-    uint4 c[8];
-    const bool inside = span * kDecSpan >= t.mis && (span + 1) * kDecSpan <= t.L;
-    if (inside) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const u32x4* a = reinterpret_cast<const u32x4*>(t.al + base + 1024 * k);
-        const u32x4 v = AMPH_XDEC_COUNT_NT ? __builtin_nontemporal_load(a) : *a;
-        c[k] = make_uint4(v.x, v.y, v.z, v.w);
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) c[k] = t.chunk((long long)(base + 1024 * k));
-    }
-    uint32_t cnt = 0, low = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      cnt += __popc(swar_colon(c[k].x)) + __popc(swar_colon(c[k].y)) + __popc(swar_colon(c[k].z)) +
-             __popc(swar_colon(c[k].w));
-      low |= swar_below21(c[k].x) | swar_below21(c[k].y) | swar_below21(c[k].z) | swar_below21(c[k].w);
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-    if ((threadIdx.x & 63) == 0) h.l0[span] = cnt;
-    gsum += cnt;
-    // whitespace (or a control byte) in a span wholly inside the text
-    ws_any |= inside && __ballot(low != 0) != 0;
-  }
-  __shared__ uint32_t wsum[kCntWaves];
-  if ((threadIdx.x & 63) == 0) wsum[wave] = gsum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t g = 0;
-#pragma unroll
-    for (int w = 0; w < kCntWaves; ++w) g += wsum[w];
-    h.l1[group] = g;
-    atomicAdd((unsigned long long*)&h.l2[group >> 6], (unsigned long long)g);
-  }
-  if (ws_any && (threadIdx.x & 63) == 0) atomicOr(&flags[0], 1u);
-}
+// Flags of one decode, zeroed with the counts before the pass (k_hier_zero):
+// [0] a workgroup gave up waiting for its predecessors' counts, [1] k_xdec_one
+// met a value outside the compact layout.  Either sends the whole text through
+// the general pass.
+constexpr int kCntWaves = 4;  // (tools/ubench/ubench_xcount.hip's count kernel shape)
 
 // The workgroup's 8 KiB span plus kWinPad bytes either side, staged in LDS;
 // bytes outside it (long whitespace runs) come from global memory.
@@ -799,8 +728,53 @@ __device__ __forceinline__ bool fast_segment(const uint32_t* l32, uint32_t o, ui
   });
 }
 
+// fast_segment without the value's global index (k_xdec_one parses before
+// its span's first index is known): the member comes from the byte before the
+// key's quote ('{' member 0, ',' member 1 -- that byte ends the previous
+// value's segment, which checks it), and the parts of the check that depend
+// on the index are returned for k_xdec_one to apply once it knows it:
+//   SEG_OK     every index-independent check held (the member's own form);
+//   SEG_M1     member 1 (the index must be odd);
+//   SEG_FIRST  the value opens the text ("[{" and the 6th byte: needed if g == 0);
+//   SEG_LAST   member 1 closing the text ("}]" and the end: needed if g + 1 == nvals);
+//   SEG_MID    member 1 followed by the next pair ("},{"K":": needed otherwise).
+enum : uint32_t { SEG_OK = 1, SEG_M1 = 2, SEG_FIRST = 4, SEG_LAST = 8, SEG_MID = 16 };
+
+__device__ __forceinline__ uint32_t fast_value(const uint32_t* l32, uint32_t o, size_t xo, size_t len,
+                                               FastNum& r) {
+  const uint32_t pre = lds_dword(l32, o - 5);  // bytes o-5 .. o-2: '{'|',' '"' k '"'
+  r.key = (pre >> 16) & 0xFFu;
+  const uint32_t lead = pre & 0xFFu;
+  const bool m1 = lead == (uint32_t)',';
+  bool ok = (pre & 0xFF00FF00u) == 0x22002200u && (r.key == 'a' || r.key == 'b') &&
+            (lead == (uint32_t)'{' || m1) && (lds_dword(l32, o - 1) & 0xFFu) == (uint32_t)':';
+  uint32_t flags = m1 ? SEG_M1 : 0;
+  if (xo == 6 && (lds_dword(l32, o - 6) & 0xFFFFu) == 0x7B5Bu) flags |= SEG_FIRST;  // "[{"
+  const uint32_t key = r.key;
+  ok = fast_parse(l32, o, ok, r, [&](uint32_t dend) {
+    const uint32_t a0 = lds_dword(l32, dend), a1 = lds_dword(l32, dend + 4);
+    if (!m1) {  // NUM ',' '"' K '"' ':', K the other key
+      const uint32_t k = (a0 >> 16) & 0xFFu;
+      return (a0 & 0xFF00FFFFu) == 0x2200222Cu && (k == 'a' || k == 'b') && k != key &&
+             (a1 & 0xFFu) == (uint32_t)':';
+    }
+    if ((a0 & 0xFFFFu) == 0x5D7Du && xo + (dend - o) + 2 == len) flags |= SEG_LAST;  // "}]" + end
+    const uint32_t k = a1 & 0xFFu;
+    if (a0 == 0x227B2C7Du && (a1 & 0x00FFFF00u) == 0x003A2200u && (k == 'a' || k == 'b')) flags |= SEG_MID;
+    return (flags & (SEG_LAST | SEG_MID)) != 0;
+  });
+  return ok ? flags | SEG_OK : flags;
+}
+
+__device__ __forceinline__ bool segment_holds(uint32_t f, uint64_t g, size_t nvals) {
+  if (!(f & SEG_OK) || g >= nvals || ((f & SEG_M1) != 0) != ((g & 1) != 0)) return false;
+  if (g == 0 && !(f & SEG_FIRST)) return false;
+  if (f & SEG_M1) return (f & (g + 1 == nvals ? SEG_LAST : SEG_MID)) != 0;
+  return true;
+}
+
 // Pass 3, general (k_xdec_slow, one workgroup per span; its workgroups
-// return at once unless k_xdec_fast found a value outside the compact
+// return at once unless k_xdec_one found a value outside the compact
 // layout): each
 // workgroup finds its colons again (from LDS), scans them to
 // global number indices and lists their positions in LDS; then its
@@ -819,7 +793,7 @@ __device__ __forceinline__ bool fast_segment(const uint32_t* l32, uint32_t o, ui
 constexpr int kMaxStarts = 1280;
 
 // Launched with a small grid (kSlowGrid workgroups), each workgroup taking
-// spans blockIdx.x, + gridDim.x, ...: when k_xdec_fast held, every workgroup
+// spans blockIdx.x, + gridDim.x, ...: when k_xdec_one held, every workgroup
 // returns at once, and 1024 of them cost ~2 us where one per span (92 k for
 // 752 MB) cost 21 us of dispatch.
 constexpr unsigned kSlowGrid = 1024;
@@ -828,7 +802,7 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_slow(Text text, Hier h, size
                                                      size_t nvals, uint4* mag, uint8_t* neg,
                                                      unsigned long long* bad,
                                                      const unsigned int* flags) {
-  if (flags[0] == 0 && flags[1] == 0) return;  // k_xdec_fast held
+  if (flags[0] == 0 && flags[1] == 0) return;  // k_xdec_one held
   __shared__ uint4 win4[kWin / 16 + 1];
   __shared__ uint16_t pos[kMaxStarts];   // start, relative to b0
   __shared__ uint16_t endp[kMaxStarts];  // one past the last digit, relative to w0
@@ -988,23 +962,76 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_slow(Text text, Hier h, size
   }
 }
 
-// Pass 3 (optimistic): the same staging and colon listing, then one value
-// per lane checked against its compact-layout SEGMENT (fast_segment) and
-// written; no whitespace walks, no records, no second phase, no general
-// path in the kernel (its registers cost occupancy: 100 SGPRs with it, 72
-// without).  Any value outside the compact layout (whitespace, a malformed
-// byte, value 0 or the last value not in the plain form, more colons than
-// expected) raises *slow, and k_xdec_slow then parses the whole text with
-// the general grammar and reports errors; Jackson's compact output never
-// takes it.
-__global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, Hier h, size_t nb,
-                                                     size_t nvals, uint4* mag, uint8_t* neg,
-                                                     unsigned int* flags) {
-  if (flags[0] != 0) return;  // whitespace somewhere: the general pass does it all
+// THE decode pass, one read of the text (k_xdec_one; one workgroup per
+// 8 KiB span).  Stage the span + kWinPad either side in LDS, list its colons
+// (one per value: "k":NUM), PUBLISH the colon count -- one agent-scope atomic
+// add each to l0[span], l1[span >> 6] and l2[span >> 12], count + kOne, onto
+// words zeroed by the launch before -- then parse one value per lane into
+// registers against its compact-layout SEGMENT (fast_segment), and only then
+// learn the span's first value index from the published counts of every span
+// before it (published_prefix: ONE wave, three polls per lane, retried
+// until every needed word carries all its contributors) and store.  A span
+// waits only for spans dispatched before it to reach their publication, which
+// each does right after its colon listing, so no chain of prefixes forms (a
+// decoupled look-back that waited for its predecessor's INCLUSIVE prefix moved
+// its frontier 64 spans per memory round trip across the eight XCDs and
+// measured 1.5-2.8x slower in round 2).  This replaced a separate count pass
+// that read the whole text once more (112 us of 405 for 752 MB).  Any value
+// outside the compact layout (whitespace, a malformed byte, value 0 or the last
+// value not in the plain form, more colons than a span can hold), or a wait
+// that gives up (kLookPolls), raises a flag and k_xdec_slow parses the whole
+// text with the general grammar and reports errors; Jackson's compact output
+// never takes it.
+constexpr int kLookPolls = 1 << 14;  // ~1 us each: a bound, never reached with in-order dispatch
+
+// A poll reads the word by an atomic add of 0 (done at the memory side, like
+// the publishing adds), not by an sc1 load: the hand-off table of
+// MI355X_MICROARCH.md lists 8-byte sc1 loads as unmeasured for this pattern.
+__device__ __forceinline__ uint64_t ld_sc1(uint64_t* p) {
+  return __hip_atomic_fetch_add(p, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// whole wave: the exclusive value prefix of span s once every span before it
+// has published its count; false if that takes more than kLookPolls polls
+__device__ __forceinline__ bool published_prefix(const Hier& h, size_t s, uint64_t* prefix) {
+  const size_t lane = __lane_id();
+  const size_t b2 = s >> 12, g0 = b2 << 6, g1 = s >> 6, s0 = g1 << 6;
+  for (int poll = 0; poll < kLookPolls; ++poll) {
+    uint64_t v = 0;
+    bool ready = true;
+    for (size_t k = lane; k < b2; k += 64) {  // whole 4096-span blocks before s's
+      const uint64_t x = ld_sc1(&h.l2[k]);
+      v += x & kCountMask;
+      ready &= (x >> 40) == 4096;
+    }
+    if (g0 + lane < g1) {  // whole 64-span groups before s's, in its block
+      const uint64_t x = ld_sc1(&h.l1[g0 + lane]);
+      v += x & kCountMask;
+      ready &= (x >> 40) == 64;
+    }
+    if (s0 + lane < s) {  // spans before s in its group
+      const uint64_t x = ld_sc1(&h.l0[s0 + lane]);
+      v += x & kCountMask;
+      ready &= (x >> 40) == 1;
+    }
+    if (__ballot(!ready) == 0) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+      *prefix = v;
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(kDecBlock) void k_xdec_one(Text text, Hier h, size_t nb, size_t nvals,
+                                                    uint4* mag, uint8_t* neg, unsigned int* flags) {
   __shared__ uint4 win4[kWin / 16 + 1];
   __shared__ uint16_t pos[kMaxStarts];  // colon, relative to b0
   __shared__ uint64_t sbase;
-  const size_t span = AMPH_XDEC_REVERSE ? nb - 1 - blockIdx.x : blockIdx.x;
+  __shared__ int sok;
+  const size_t span = blockIdx.x;
   const size_t b0 = span * kDecSpan;
   const long long w0 = (long long)b0 - kWinPad;
   if (w0 >= (long long)text.mis && w0 + 16LL * (kWin / 16 + 1) <= (long long)text.L) {
@@ -1022,10 +1049,6 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, Hier h, size
   } else {
     for (int c = threadIdx.x; c < kWin / 16 + 1; c += kDecBlock) win4[c] = text.chunk(w0 + 16LL * c);
   }
-  if (threadIdx.x < 64) {  // the span's first value index, beside the text loads
-    const uint64_t b = hier_prefix(h, span);
-    if (threadIdx.x == 0) sbase = b;
-  }
   __syncthreads();
   const int lo = kWinPad + kDecBytes * threadIdx.x;
   const uint4 c0 = win4[lo / 16], c1 = win4[lo / 16 + 1];
@@ -1033,27 +1056,71 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, Hier h, size
   uint32_t m = colons32(w);
   uint32_t total;
   const uint32_t first = block_excl_scan32(__popc(m), &total);
+  if (threadIdx.x == 0) {  // publish this span's count (colons: one per value)
+    atomicAdd((unsigned long long*)&h.l0[span], (unsigned long long)(total + kOne));
+    atomicAdd((unsigned long long*)&h.l1[span >> 6], (unsigned long long)(total + kOne));
+    atomicAdd((unsigned long long*)&h.l2[span >> 12], (unsigned long long)(total + kOne));
+  }
   for (int k = (int)first; m && k < kMaxStarts; m &= m - 1, ++k)
     pos[k] = (uint16_t)(kDecBytes * threadIdx.x + __ffs(m) - 1);
   __syncthreads();
   bool fail = total > (uint32_t)kMaxStarts;
   const uint32_t nloc = min(total, (uint32_t)kMaxStarts);
-  const uint64_t gbase = sbase;
   const uint32_t* l32 = reinterpret_cast<const uint32_t*>(win4);
   const size_t len = text.L - text.mis;
-  for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
-    const uint32_t at = pos[idx];
-    const uint64_t g = gbase + idx;
+  // the span's first value index: wave 0 learns it after its own values are
+  // parsed (the wait overlaps the other waves' parse and the CU's other
+  // workgroups); a span with more values than lanes learns it first
+  auto learn_base = [&]() {
+    if (threadIdx.x < 64) {
+      uint64_t b = 0;
+      const bool ok = published_prefix(h, span, &b);
+      if (threadIdx.x == 0) {
+        sbase = b;
+        sok = ok;
+      }
+    }
+    __syncthreads();
+  };
+  if (nloc <= (uint32_t)kDecBlock) {
+    const uint32_t idx = threadIdx.x;
     FastNum fn;
-    if (g < nvals && fast_segment(l32, at + 1 + kWinPad, g, nvals, b0 + at + 1 - text.mis, len, fn)) {
-      const size_t slot = (g & ~(uint64_t)1) + (fn.key == 'b');
-      xst16(mag + slot, make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]));
-      neg[slot] = fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0;
-    } else {
+    uint32_t f = 0;
+    if (idx < nloc) {
+      const uint32_t at = pos[idx];
+      f = fast_value(l32, at + 1 + kWinPad, b0 + at + 1 - text.mis, len, fn);
+    }
+    learn_base();
+    if (!sok) {
       fail = true;
+    } else if (idx < nloc) {
+      const uint64_t g = sbase + idx;
+      if (segment_holds(f, g, nvals)) {
+        const size_t slot = (g & ~(uint64_t)1) + (fn.key == 'b');
+        xst16(mag + slot, make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]));
+        neg[slot] = fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0;
+      } else {
+        fail = true;
+      }
+    }
+  } else {
+    learn_base();
+    if (!sok) fail = true;
+    for (uint32_t idx = threadIdx.x; idx < nloc && sok; idx += kDecBlock) {
+      const uint32_t at = pos[idx];
+      const uint64_t g = sbase + idx;
+      FastNum fn;
+      const uint32_t f = fast_value(l32, at + 1 + kWinPad, b0 + at + 1 - text.mis, len, fn);
+      if (segment_holds(f, g, nvals)) {
+        const size_t slot = (g & ~(uint64_t)1) + (fn.key == 'b');
+        xst16(mag + slot, make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]));
+        neg[slot] = fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0;
+      } else {
+        fail = true;
+      }
     }
   }
-  if (__ballot(fail) != 0 && __lane_id() == 0) atomicOr(&flags[1], 1u);
+  if (__ballot(fail) != 0 && __lane_id() == 0) atomicOr(&flags[sok ? 1 : 0], 1u);
 }
 
 // The array holds exactly nvals numbers and is bracketed; an empty array
@@ -1138,9 +1205,8 @@ size_t xdec_scratch_bytes(size_t len) {  // span counts, the l1 / l2 sums, the t
   return 8 * (nb + blocks_of(nb, kGroupSpans) + blocks_of(nb, (size_t)kGroupSpans * 64) + 1);
 }
 
-// zero the l2 sums and flags, count (+ l0/l1/l2), the compact pass, the
-// general pass (returns at once unless the compact pass could not hold), the
-// array check: five launches.
+// zero the counts and flags, the single pass, the general pass (returns at
+// once unless the single pass could not hold), the array check: four launches.
 hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, uint4* mag,
                                   uint8_t* neg, unsigned long long* bad, void* scratch,
                                   const LaunchCfg& c) {
@@ -1148,14 +1214,14 @@ hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, u
   const Text t{reinterpret_cast<const uint8_t*>(text) - mis, mis, mis + len};
   const size_t nb = blocks_of(t.L ? t.L : 1, kDecSpan);
   const XdecScratch x = xdec_layout(scratch, nb);
+  const size_t nwords = nb + blocks_of(nb, kGroupSpans) + blocks_of(nb, (size_t)kGroupSpans * 64);
   LaunchCfg c0 = c, cm = c, c1 = c;
   c0.ev_stop = nullptr;
   cm.ev_start = cm.ev_stop = nullptr;
   c1.ev_start = nullptr;
-  AMPH_LAUNCH(k_hier_zero, dim3(1), dim3(256), c0, x.h.l2, blocks_of(nb, (size_t)kGroupSpans * 64), x.flags, 2);
-  AMPH_LAUNCH(k_xdec_count, dim3((unsigned)blocks_of(nb, kGroupSpans)), dim3(64 * kCntWaves), cm, t, x.h, nb,
-              x.flags);
-  AMPH_LAUNCH(k_xdec_fast, dim3((unsigned)nb), dim3(kDecBlock), cm, t, x.h, nb, 2 * npairs, mag, neg, x.flags);
+  AMPH_LAUNCH(k_hier_zero, dim3(std::min<unsigned>(blocks_of(nwords, 256), 256u)), dim3(256), c0, x.h.l0, nwords,
+              x.flags, 2);
+  AMPH_LAUNCH(k_xdec_one, dim3((unsigned)nb), dim3(kDecBlock), cm, t, x.h, nb, 2 * npairs, mag, neg, x.flags);
   AMPH_LAUNCH(k_xdec_slow, dim3((unsigned)std::min<size_t>(nb, kSlowGrid)), dim3(kDecBlock), cm, t, x.h, nb,
               2 * npairs, mag, neg, bad, (const unsigned int*)x.flags);
   AMPH_LAUNCH(k_xdec_check, dim3(1), dim3(256), c1, t, x.h, nb, 2 * npairs, bad);
