@@ -28,6 +28,8 @@
 // 64-by-32-bit divisions by a constant in all, to_chunks), chunks <-> digits.
 #include <hip/hip_ext.h>
 
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace amph {
@@ -51,6 +53,7 @@ __device__ __forceinline__ void xst16(uint4* p, uint4 v) {
 
 constexpr int kXBlock = 256;      // pairs per workgroup (encode)
 constexpr int kXEntry = 92;       // max entry: {"a":-<39 digits>,"b":-<39 digits>},
+constexpr int kScanBlock = 1024;  // elements per workgroup of the scan passes
 constexpr int kDecBytes = 32;     // text bytes per lane (decode)
 constexpr uint64_t kE9 = 1000000000ull;
 
@@ -207,7 +210,38 @@ __device__ __forceinline__ char* put_digits(char* o, const uint32_t (&ch)[5], in
   return o + nd;
 }
 
-// ---- workgroup scans ----------------------------------------------------------------
+// ---- device-wide exclusive scan of u64 (three passes) ----------------------------
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+  const int lane = __lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// Exclusive scan over the workgroup (blockDim multiple of 64, <= 1024);
+// returns this lane's exclusive prefix, *total = the workgroup sum.
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* total) {
+  __shared__ uint64_t wsum[17];  // 16 wave offsets + the total
+  const int lane = __lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint64_t inc = wave_incl_scan(v);
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  if (wave == 0) {
+    const uint64_t s = lane < nw ? wsum[lane] : 0;
+    const uint64_t si = wave_incl_scan(s);
+    if (lane < nw) wsum[lane] = si - s;  // exclusive wave offsets
+    if (lane == nw - 1) wsum[16] = si;
+  }
+  __syncthreads();
+  const uint64_t r = wsum[wave] + inc - v;
+  *total = wsum[16];
+  __syncthreads();
+  return r;
+}
+
 // Inclusive wave scan of 32-bit values with DPP: row_shr 1/2/4/8 scans each
 // 16-lane row, row_bcast 15/31 carries the row totals (6 VALU with DPP
 // operands where a __shfl_up ladder costs ~40 VALU and six ds_bpermute).
@@ -242,97 +276,62 @@ __device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t* tota
   return r;
 }
 
-// ---- hierarchical counts: per-unit bases without scan passes -----------------
-// Unit s's count in l0[s] (a decode span's values, an encode block's text
-// bytes); l1[s >> 6] = the sum of its 64-unit group (written by the one
-// workgroup that counts the group); l2[s >> 12] = the sum of 4096 units (64
-// groups; agent-scope atomic adds onto words zeroed by a launch before).  The
-// exclusive prefix of unit s is then three masked loads per lane of ONE wave
-// and a wave reduction -- l2 below s's 4096-block, l1 of the groups before s
-// in it, l0 of the units before s in its group -- issued beside the unit's
-// own loads.  This replaced a three-launch scan of the counts (k_scan_reduce
-// / single / apply, ~5 us each, mostly launch latency).
-struct Hier {
-  uint64_t* l0;
-  uint64_t* l1;
-  uint64_t* l2;
-};
-constexpr int kGroupSpans = 64;  // units per l1 group = per counting workgroup
-
-// Counts live in bits 0..39 of the words; the decode's single pass marks
-// each publication in bits 40..63 (kOne per contributor, see k_xdec_one).
-constexpr uint64_t kOne = 1ull << 40, kCountMask = kOne - 1;
-
-// call with a whole wave; every lane returns the prefix
-__device__ __forceinline__ uint64_t hier_prefix(const Hier& h, size_t s) {
-  const size_t lane = __lane_id();
-  uint64_t v = 0;
-  for (size_t k = lane; k < (s >> 12); k += 64) v += h.l2[k] & kCountMask;
-  const size_t g0 = (s >> 12) << 6, g1 = s >> 6;
-  if (g0 + lane < g1) v += h.l1[g0 + lane] & kCountMask;
-  const size_t s0 = (s >> 6) << 6;
-  if (s0 + lane < s) v += h.l0[s0 + lane] & kCountMask;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+__global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const uint64_t* x, size_t n,
+                                                        uint64_t* bsum) {
+  const size_t i = (size_t)blockIdx.x * kScanBlock + threadIdx.x;
+  uint64_t total;
+  block_excl_scan(i < n ? x[i] : 0, &total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-// every unit's count: one wave
-__device__ __forceinline__ uint64_t hier_total(const Hier& h, size_t n) {
-  uint64_t v = 0;
-  for (size_t k = __lane_id(); k < ((n + 4095) >> 12); k += 64) v += h.l2[k] & kCountMask;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// One workgroup: in-place exclusive scan of n values, x[n] = total.
+__global__ __launch_bounds__(kScanBlock) void k_scan_single(uint64_t* x, size_t n) {
+  uint64_t carry = 0;
+  for (size_t base = 0; base < n; base += kScanBlock) {
+    const size_t i = base + threadIdx.x;
+    const uint64_t v = i < n ? x[i] : 0;
+    uint64_t total;
+    const uint64_t e = block_excl_scan(v, &total);
+    if (i < n) x[i] = carry + e;
+    carry += total;
+  }
+  if (threadIdx.x == 0) x[n] = carry;
 }
 
-__global__ __launch_bounds__(256) void k_hier_zero(uint64_t* w, size_t n, unsigned int* flags, int nflags) {
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) w[i] = 0;
-  if (blockIdx.x == 0 && (int)threadIdx.x < nflags) flags[threadIdx.x] = 0;
+// x[i] <- exclusive prefix (bsum already scanned); x[n] <- total
+__global__ __launch_bounds__(kScanBlock) void k_scan_apply(uint64_t* x, size_t n,
+                                                       const uint64_t* bsum, size_t nb) {
+  const size_t i = (size_t)blockIdx.x * kScanBlock + threadIdx.x;
+  uint64_t total;
+  const uint64_t e = block_excl_scan(i < n ? x[i] : 0, &total);
+  if (i < n) x[i] = bsum[blockIdx.x] + e;
+  if (blockIdx.x == 0 && threadIdx.x == 0) x[n] = bsum[nb];
 }
 
-// Encode pass 1: the text length of each 256-pair block's run of entries
-// (l0[b] = sum of the entry lengths of pairs [256 b, 256 b + 256)) and the
-// l1 / l2 sums of the hierarchy; digit counts from the bit length
-// (ndigits128), not the base-10^9 split.  One workgroup per 64 blocks: 16
-// rounds of one pair per lane, 4 blocks of 256 pairs per 1024-lane round --
-// wave sums by shuffles, then 4 lanes add their block's 4 wave sums.
+// Encode pass 1: the text length of each workgroup's run of entries
+// (bs[g] = sum of the entry lengths of pairs [256 g, 256 g + 256)); digit
+// counts from the bit length (ndigits128), not the base-10^9 split.
 __global__ __launch_bounds__(4 * kXBlock) void k_xenc_bsum(const uint4* mag, const uint8_t* neg,
-                                                       size_t npairs, size_t nb, Hier h) {
+                                                       size_t npairs, size_t nb, uint64_t* bs) {
+  // one pair per lane, 4 sub-blocks of 256 pairs per 1024-lane workgroup:
+  // wave sums by shuffles, then 4 lanes add their sub-block's 4 wave sums
   __shared__ uint32_t ws[16];
-  uint32_t gsum = 0;  // lanes 0..3: their blocks' lengths over the rounds
-  for (int round = 0; round < kGroupSpans / 4; ++round) {
-    const size_t b4 = (size_t)blockIdx.x * kGroupSpans + 4 * round;  // this round's first block
-    if (b4 >= nb) break;
-    const size_t k = b4 * kXBlock + threadIdx.x;
-    uint32_t len = 0;
-    if (k < npairs) {  // {"a":A,"b":B} (+ ',' unless last)
-      const uint4 d = mag[2 * k], e = mag[2 * k + 1];
-      len = 11 + ndigits128(d) + (neg[2 * k] != 0 && !is_zero(d)) + ndigits128(e) +
-            (neg[2 * k + 1] != 0 && !is_zero(e)) + (k + 1 < npairs);
-    }
+  const size_t k = (size_t)blockIdx.x * (4 * kXBlock) + threadIdx.x;
+  uint32_t len = 0;
+  if (k < npairs)
+  {  // {"a":A,"b":B} (+ ',' unless last)
+    const uint4 d = mag[2 * k], e = mag[2 * k + 1];
+    len = 11 + ndigits128(d) + (neg[2 * k] != 0 && !is_zero(d)) + ndigits128(e) +
+          (neg[2 * k + 1] != 0 && !is_zero(e)) + (k + 1 < npairs);
+  }
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) len += __shfl_xor(len, o, 64);
-    if (__lane_id() == 0) ws[threadIdx.x >> 6] = len;
-    __syncthreads();
-    const size_t sub = b4 + threadIdx.x;
-    if (threadIdx.x < 4 && sub < nb) {
-      const uint32_t b = ws[4 * threadIdx.x] + ws[4 * threadIdx.x + 1] + ws[4 * threadIdx.x + 2] +
-                         ws[4 * threadIdx.x + 3];
-      h.l0[sub] = b;
-      gsum += b;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x < 64) {
-    uint32_t g = threadIdx.x < 4 ? gsum : 0;
-    g += __shfl_xor(g, 1, 64);
-    g += __shfl_xor(g, 2, 64);
-    if (threadIdx.x == 0) {
-      h.l1[blockIdx.x] = g;
-      atomicAdd((unsigned long long*)&h.l2[blockIdx.x >> 6], (unsigned long long)g);
-    }
-  }
+  for (int o = 32; o >= 1; o >>= 1) len += __shfl_xor(len, o, 64);
+  if (__lane_id() == 0) ws[threadIdx.x >> 6] = len;
+  __syncthreads();
+  const size_t sub = 4 * (size_t)blockIdx.x + threadIdx.x;
+  if (threadIdx.x < 4 && sub < nb)
+    bs[sub] = (uint64_t)ws[4 * threadIdx.x] + ws[4 * threadIdx.x + 1] + ws[4 * threadIdx.x + 2] +
+              ws[4 * threadIdx.x + 3];
 }
 
 // Encode pass 3 (after the scan of bs): each lane converts its two numbers,
@@ -342,19 +341,10 @@ __global__ __launch_bounds__(4 * kXBlock) void k_xenc_bsum(const uint4* mag, con
 // wholly inside it moves as one aligned ds_read_b128 + global 16-byte store;
 // the up to 15 bytes at either end go out singly.
 __global__ __launch_bounds__(kXBlock) void k_xenc_write(const uint4* mag, const uint8_t* neg,
-                                                    size_t npairs, Hier h,
+                                                    size_t npairs, const uint64_t* bs,
                                                     size_t nblocks, char* out,
                                                     unsigned long long* out_len) {
   __shared__ uint4 bufv[(kXBlock * kXEntry + 8) / 16 + 2];
-  __shared__ uint64_t sbase, stotal;
-  if (threadIdx.x < 64) {  // this block's text offset (and block 0: the whole text's length)
-    const uint64_t b = hier_prefix(h, blockIdx.x);
-    const uint64_t t = blockIdx.x == 0 ? hier_total(h, nblocks) : 0;
-    if (threadIdx.x == 0) {
-      sbase = b;
-      stotal = t;
-    }
-  }
   char* buf = reinterpret_cast<char*>(bufv);
   const size_t k = (size_t)blockIdx.x * kXBlock + threadIdx.x;
   uint32_t cd[5], ce[5];
@@ -369,8 +359,8 @@ __global__ __launch_bounds__(kXBlock) void k_xenc_write(const uint4* mag, const 
     se = neg[2 * k + 1] != 0 && !is_zero(e);
     len = 11 + nd + sd + ne + se + (k + 1 < npairs);
   }
-  const uint32_t loc = block_excl_scan32(len, &total);  // its barriers publish sbase / stotal
-  const uint64_t base = sbase;
+  const uint32_t loc = block_excl_scan32(len, &total);
+  const uint64_t base = bs[blockIdx.x];
   char* dst = out + 1 + base;  // out[0] = '['
   const size_t sh = (uintptr_t)dst & 15;
   if (k < npairs) {
@@ -398,8 +388,8 @@ __global__ __launch_bounds__(kXBlock) void k_xenc_write(const uint4* mag, const 
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     out[0] = '[';
-    out[1 + stotal] = ']';
-    if (out_len) *out_len = stotal + 2;
+    out[1 + bs[nblocks]] = ']';
+    if (out_len) *out_len = bs[nblocks] + 2;
   }
 }
 
@@ -472,11 +462,51 @@ constexpr size_t kDecSpan = (size_t)kDecBlock * kDecBytes;  // 8 KiB of text per
 constexpr int kWinPad = 256;                           // window context either side
 constexpr int kWin = (int)kDecSpan + 2 * kWinPad;      // staged bytes
 
-// Flags of one decode, zeroed with the counts before the pass (k_hier_zero):
-// [0] a workgroup gave up waiting for its predecessors' counts, [1] k_xdec_one
-// met a value outside the compact layout.  Either sends the whole text through
-// the general pass.
-constexpr int kCntWaves = 4;  // (tools/ubench/ubench_xcount.hip's count kernel shape)
+// Pass 1: colons (= numbers) per 8 KiB span, ONE WAVE PER SPAN: 64 lanes x
+// eight 16-B loads in flight, lane-interleaved so that every wave
+// instruction reads 1 KiB contiguous (nontemporal: the text is read once here
+// and once by the parse), a wave reduction, no LDS or barrier; four spans per
+// 256-lane workgroup.  96 us per 640 MB text where 128 lanes x 64
+// lane-contiguous bytes per span took 162 (tools/ubench/ubench_xcount.hip).
+constexpr int kCntWaves = 4;
+// bsum / bscan words: colon count in bits 0..39, spans with whitespace from bit 40
+constexpr uint64_t kWsBit = 1ull << 40, kCountMask = kWsBit - 1;
+
+__device__ __forceinline__ uint32_t swar_below21(uint32_t w) {  // nonzero iff some byte < 0x21
+  return (w - 0x21212121u) & ~w & 0x80808080u;
+}
+
+__global__ __launch_bounds__(64 * kCntWaves) void k_xdec_count(Text t, uint64_t* bsum, size_t nb,
+                                                             unsigned int* slow) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *slow = 0;  // k_xdec_fast's flag
+  const size_t span = (size_t)blockIdx.x * kCntWaves + (threadIdx.x >> 6);
+  if (span >= nb) return;
+  const size_t base = span * kDecSpan + (size_t)(threadIdx.x & 63) * 16;
+  uint4 c[8];
+  if (span * kDecSpan >= t.mis && (span + 1) * kDecSpan <= t.L) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(t.al + base + 1024 * k));
+      c[k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = t.chunk((long long)(base + 1024 * k));
+  }
+  uint32_t cnt = 0, low = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    cnt += __popc(swar_colon(c[k].x)) + __popc(swar_colon(c[k].y)) + __popc(swar_colon(c[k].z)) +
+           __popc(swar_colon(c[k].w));
+    low |= swar_below21(c[k].x) | swar_below21(c[k].y) | swar_below21(c[k].z) | swar_below21(c[k].w);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  // whitespace (or a control byte) in a span wholly inside the text: the
+  // compact fast pass cannot hold, so it is skipped (kWsBit, summed by the scan)
+  const bool ws = span * kDecSpan >= t.mis && (span + 1) * kDecSpan <= t.L && __ballot(low != 0) != 0;
+  if ((threadIdx.x & 63) == 0) bsum[span] = cnt | (ws ? kWsBit : 0);
+}
 
 // The workgroup's 8 KiB span plus kWinPad bytes either side, staged in LDS;
 // bytes outside it (long whitespace runs) come from global memory.
@@ -728,53 +758,8 @@ __device__ __forceinline__ bool fast_segment(const uint32_t* l32, uint32_t o, ui
   });
 }
 
-// fast_segment without the value's global index (k_xdec_one parses before
-// its span's first index is known): the member comes from the byte before the
-// key's quote ('{' member 0, ',' member 1 -- that byte ends the previous
-// value's segment, which checks it), and the parts of the check that depend
-// on the index are returned for k_xdec_one to apply once it knows it:
-//   SEG_OK     every index-independent check held (the member's own form);
-//   SEG_M1     member 1 (the index must be odd);
-//   SEG_FIRST  the value opens the text ("[{" and the 6th byte: needed if g == 0);
-//   SEG_LAST   member 1 closing the text ("}]" and the end: needed if g + 1 == nvals);
-//   SEG_MID    member 1 followed by the next pair ("},{"K":": needed otherwise).
-enum : uint32_t { SEG_OK = 1, SEG_M1 = 2, SEG_FIRST = 4, SEG_LAST = 8, SEG_MID = 16 };
-
-__device__ __forceinline__ uint32_t fast_value(const uint32_t* l32, uint32_t o, size_t xo, size_t len,
-                                               FastNum& r) {
-  const uint32_t pre = lds_dword(l32, o - 5);  // bytes o-5 .. o-2: '{'|',' '"' k '"'
-  r.key = (pre >> 16) & 0xFFu;
-  const uint32_t lead = pre & 0xFFu;
-  const bool m1 = lead == (uint32_t)',';
-  bool ok = (pre & 0xFF00FF00u) == 0x22002200u && (r.key == 'a' || r.key == 'b') &&
-            (lead == (uint32_t)'{' || m1) && (lds_dword(l32, o - 1) & 0xFFu) == (uint32_t)':';
-  uint32_t flags = m1 ? SEG_M1 : 0;
-  if (xo == 6 && (lds_dword(l32, o - 6) & 0xFFFFu) == 0x7B5Bu) flags |= SEG_FIRST;  // "[{"
-  const uint32_t key = r.key;
-  ok = fast_parse(l32, o, ok, r, [&](uint32_t dend) {
-    const uint32_t a0 = lds_dword(l32, dend), a1 = lds_dword(l32, dend + 4);
-    if (!m1) {  // NUM ',' '"' K '"' ':', K the other key
-      const uint32_t k = (a0 >> 16) & 0xFFu;
-      return (a0 & 0xFF00FFFFu) == 0x2200222Cu && (k == 'a' || k == 'b') && k != key &&
-             (a1 & 0xFFu) == (uint32_t)':';
-    }
-    if ((a0 & 0xFFFFu) == 0x5D7Du && xo + (dend - o) + 2 == len) flags |= SEG_LAST;  // "}]" + end
-    const uint32_t k = a1 & 0xFFu;
-    if (a0 == 0x227B2C7Du && (a1 & 0x00FFFF00u) == 0x003A2200u && (k == 'a' || k == 'b')) flags |= SEG_MID;
-    return (flags & (SEG_LAST | SEG_MID)) != 0;
-  });
-  return ok ? flags | SEG_OK : flags;
-}
-
-__device__ __forceinline__ bool segment_holds(uint32_t f, uint64_t g, size_t nvals) {
-  if (!(f & SEG_OK) || g >= nvals || ((f & SEG_M1) != 0) != ((g & 1) != 0)) return false;
-  if (g == 0 && !(f & SEG_FIRST)) return false;
-  if (f & SEG_M1) return (f & (g + 1 == nvals ? SEG_LAST : SEG_MID)) != 0;
-  return true;
-}
-
 // Pass 3, general (k_xdec_slow, one workgroup per span; its workgroups
-// return at once unless k_xdec_one found a value outside the compact
+// return at once unless k_xdec_fast found a value outside the compact
 // layout): each
 // workgroup finds its colons again (from LDS), scans them to
 // global number indices and lists their positions in LDS; then its
@@ -792,17 +777,34 @@ __device__ __forceinline__ bool segment_holds(uint32_t f, uint64_t g, size_t nva
 // a colon beyond that is reported as malformed.
 constexpr int kMaxStarts = 1280;
 
-// Launched with a small grid (kSlowGrid workgroups), each workgroup taking
-// spans blockIdx.x, + gridDim.x, ...: when k_xdec_one held, every workgroup
-// returns at once, and 1024 of them cost ~2 us where one per span (92 k for
-// 752 MB) cost 21 us of dispatch.
-constexpr unsigned kSlowGrid = 1024;
+// Launched on at most kSlowGrid workgroups, each taking spans blockIdx.x,
+// + gridDim.x, ...: when the compact pass held, every workgroup returns at
+// once, and its dispatch cost is that grid's.  One workgroup per span (92 k
+// for 752 MB) cost 21 us of dispatch just to return; 16 k cost ~5 us.  The
+// general pass itself (whitespace in the text) then runs 1.38x slower than on
+// one workgroup per span (979 vs 710 us on 752 MB; 1 k workgroups: 1285,
+// 4 k: 1058; r03 xdec A/B, profiles/r03_xdec_ab.txt).
+#ifndef AMPH_XDEC_SLOW_GRID
+#define AMPH_XDEC_SLOW_GRID 16384
+#endif
+constexpr unsigned kSlowGrid = AMPH_XDEC_SLOW_GRID;
 
-__global__ __launch_bounds__(kDecBlock) void k_xdec_slow(Text text, Hier h, size_t nb,
+// Span bases of the general pass: from the count pass's scan.
+struct ScanBases {
+  const uint64_t* bscan;
+  size_t nb;
+  __device__ __forceinline__ bool skip(const unsigned int* slow) const {
+    return *slow == 0 && (bscan[nb] & ~kCountMask) == 0;
+  }
+  __device__ __forceinline__ uint64_t base(size_t span) const { return bscan[span] & kCountMask; }
+};
+
+template <class Bases>
+__global__ __launch_bounds__(kDecBlock) void k_xdec_slow(Text text, Bases bs, size_t nb,
                                                      size_t nvals, uint4* mag, uint8_t* neg,
                                                      unsigned long long* bad,
-                                                     const unsigned int* flags) {
-  if (flags[0] == 0 && flags[1] == 0) return;  // k_xdec_one held
+                                                     const unsigned int* slow) {
+  if (bs.skip(slow)) return;  // the compact pass held
   __shared__ uint4 win4[kWin / 16 + 1];
   __shared__ uint16_t pos[kMaxStarts];   // start, relative to b0
   __shared__ uint16_t endp[kMaxStarts];  // one past the last digit, relative to w0
@@ -814,7 +816,7 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_slow(Text text, Hier h, size
   const long long w0 = (long long)b0 - kWinPad;
   for (int c = threadIdx.x; c < kWin / 16 + 1; c += kDecBlock) win4[c] = text.chunk(w0 + 16LL * c);
   if (threadIdx.x < 64) {
-    const uint64_t b = hier_prefix(h, span);
+    const uint64_t b = bs.base(span);
     if (threadIdx.x == 0) sbase = b;
   }
   __syncthreads();
@@ -962,77 +964,22 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_slow(Text text, Hier h, size
   }
 }
 
-// THE decode pass, one read of the text (k_xdec_one; one workgroup per
-// 8 KiB span).  Stage the span + kWinPad either side in LDS, list its colons
-// (one per value: "k":NUM), PUBLISH the colon count -- one agent-scope atomic
-// add each to l0[span], l1[span >> 6] and l2[span >> 12], count + kOne, onto
-// words zeroed by the launch before -- then parse one value per lane into
-// registers against its compact-layout SEGMENT (fast_segment), and only then
-// learn the span's first value index from the published counts of every span
-// before it (published_prefix: ONE wave, three polls per lane, retried
-// until every needed word carries all its contributors) and store.  A span
-// waits only for spans dispatched before it to reach their publication, which
-// each does right after its colon listing, so no chain of prefixes forms (a
-// decoupled look-back that waited for its predecessor's INCLUSIVE prefix moved
-// its frontier 64 spans per memory round trip across the eight XCDs and
-// measured 1.5-2.8x slower in round 2).  This replaced a separate count pass
-// that read the whole text once more (112 us of 405 for 752 MB).  Any value
-// outside the compact layout (whitespace, a malformed byte, value 0 or the last
-// value not in the plain form, more colons than a span can hold), or a wait
-// that gives up (kLookPolls), raises a flag and k_xdec_slow parses the whole
-// text with the general grammar and reports errors; Jackson's compact output
-// never takes it.
-constexpr int kLookPolls = 1 << 14;  // ~1 us each: a bound, never reached with in-order dispatch
-
-// A poll reads the word by an atomic add of 0 (done at the memory side, like
-// the publishing adds), not by an sc1 load: the hand-off table of
-// MI355X_MICROARCH.md lists 8-byte sc1 loads as unmeasured for this pattern.
-__device__ __forceinline__ uint64_t ld_sc1(uint64_t* p) {
-  return __hip_atomic_fetch_add(p, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// whole wave: the exclusive value prefix of span s once every span before it
-// has published its count; false if that takes more than kLookPolls polls
-__device__ __forceinline__ bool published_prefix(const Hier& h, size_t s, uint64_t* prefix) {
-  const size_t lane = __lane_id();
-  const size_t b2 = s >> 12, g0 = b2 << 6, g1 = s >> 6, s0 = g1 << 6;
-  for (int poll = 0; poll < kLookPolls; ++poll) {
-    uint64_t v = 0;
-    bool ready = true;
-    for (size_t k = lane; k < b2; k += 64) {  // whole 4096-span blocks before s's
-      const uint64_t x = ld_sc1(&h.l2[k]);
-      v += x & kCountMask;
-      ready &= (x >> 40) == 4096;
-    }
-    if (g0 + lane < g1) {  // whole 64-span groups before s's, in its block
-      const uint64_t x = ld_sc1(&h.l1[g0 + lane]);
-      v += x & kCountMask;
-      ready &= (x >> 40) == 64;
-    }
-    if (s0 + lane < s) {  // spans before s in its group
-      const uint64_t x = ld_sc1(&h.l0[s0 + lane]);
-      v += x & kCountMask;
-      ready &= (x >> 40) == 1;
-    }
-    if (__ballot(!ready) == 0) {
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-      *prefix = v;
-      return true;
-    }
-    __builtin_amdgcn_s_sleep(8);
-  }
-  return false;
-}
-
-__global__ __launch_bounds__(kDecBlock) void k_xdec_one(Text text, Hier h, size_t nb, size_t nvals,
-                                                    uint4* mag, uint8_t* neg, unsigned int* flags) {
+// Pass 3 (optimistic): the same staging and colon listing, then one value
+// per lane checked against its compact-layout SEGMENT (fast_segment) and
+// written; no whitespace walks, no records, no second phase, no general
+// path in the kernel (its registers cost occupancy: 100 SGPRs with it, 72
+// without).  Any value outside the compact layout (whitespace, a malformed
+// byte, value 0 or the last value not in the plain form, more colons than
+// expected) raises *slow, and k_xdec_slow then parses the whole text with
+// the general grammar and reports errors; Jackson's compact output never
+// takes it.
+__global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64_t* bscan, size_t nb,
+                                                     size_t nvals, uint4* mag, uint8_t* neg,
+                                                     unsigned int* slow) {
+  if ((bscan[nb] & ~kCountMask) != 0) return;  // whitespace somewhere: the general pass does it all
   __shared__ uint4 win4[kWin / 16 + 1];
   __shared__ uint16_t pos[kMaxStarts];  // colon, relative to b0
-  __shared__ uint64_t sbase;
-  __shared__ int sok;
-  const size_t span = blockIdx.x;
-  const size_t b0 = span * kDecSpan;
+  const size_t b0 = (size_t)blockIdx.x * kDecSpan;
   const long long w0 = (long long)b0 - kWinPad;
   if (w0 >= (long long)text.mis && w0 + 16LL * (kWin / 16 + 1) <= (long long)text.L) {
     // a window wholly inside the text: its 545 chunks as three plain 16-byte
@@ -1056,81 +1003,44 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_one(Text text, Hier h, size_
   uint32_t m = colons32(w);
   uint32_t total;
   const uint32_t first = block_excl_scan32(__popc(m), &total);
-  if (threadIdx.x == 0) {  // publish this span's count (colons: one per value)
-    atomicAdd((unsigned long long*)&h.l0[span], (unsigned long long)(total + kOne));
-    atomicAdd((unsigned long long*)&h.l1[span >> 6], (unsigned long long)(total + kOne));
-    atomicAdd((unsigned long long*)&h.l2[span >> 12], (unsigned long long)(total + kOne));
-  }
   for (int k = (int)first; m && k < kMaxStarts; m &= m - 1, ++k)
     pos[k] = (uint16_t)(kDecBytes * threadIdx.x + __ffs(m) - 1);
   __syncthreads();
   bool fail = total > (uint32_t)kMaxStarts;
   const uint32_t nloc = min(total, (uint32_t)kMaxStarts);
+  const uint64_t gbase = bscan[blockIdx.x] & kCountMask;
   const uint32_t* l32 = reinterpret_cast<const uint32_t*>(win4);
   const size_t len = text.L - text.mis;
-  // the span's first value index: wave 0 learns it after its own values are
-  // parsed (the wait overlaps the other waves' parse and the CU's other
-  // workgroups); a span with more values than lanes learns it first
-  auto learn_base = [&]() {
-    if (threadIdx.x < 64) {
-      uint64_t b = 0;
-      const bool ok = published_prefix(h, span, &b);
-      if (threadIdx.x == 0) {
-        sbase = b;
-        sok = ok;
-      }
-    }
-    __syncthreads();
-  };
-  if (nloc <= (uint32_t)kDecBlock) {
-    const uint32_t idx = threadIdx.x;
+  for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
+    const uint32_t at = pos[idx];
+    const uint64_t g = gbase + idx;
     FastNum fn;
-    uint32_t f = 0;
-    if (idx < nloc) {
-      const uint32_t at = pos[idx];
-      f = fast_value(l32, at + 1 + kWinPad, b0 + at + 1 - text.mis, len, fn);
-    }
-    learn_base();
-    if (!sok) {
+    if (g < nvals && fast_segment(l32, at + 1 + kWinPad, g, nvals, b0 + at + 1 - text.mis, len, fn)) {
+      const size_t slot = (g & ~(uint64_t)1) + (fn.key == 'b');
+      xst16(mag + slot, make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]));
+      neg[slot] = fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0;
+    } else {
       fail = true;
-    } else if (idx < nloc) {
-      const uint64_t g = sbase + idx;
-      if (segment_holds(f, g, nvals)) {
-        const size_t slot = (g & ~(uint64_t)1) + (fn.key == 'b');
-        xst16(mag + slot, make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]));
-        neg[slot] = fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0;
-      } else {
-        fail = true;
-      }
-    }
-  } else {
-    learn_base();
-    if (!sok) fail = true;
-    for (uint32_t idx = threadIdx.x; idx < nloc && sok; idx += kDecBlock) {
-      const uint32_t at = pos[idx];
-      const uint64_t g = sbase + idx;
-      FastNum fn;
-      const uint32_t f = fast_value(l32, at + 1 + kWinPad, b0 + at + 1 - text.mis, len, fn);
-      if (segment_holds(f, g, nvals)) {
-        const size_t slot = (g & ~(uint64_t)1) + (fn.key == 'b');
-        xst16(mag + slot, make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]));
-        neg[slot] = fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0;
-      } else {
-        fail = true;
-      }
     }
   }
-  if (__ballot(fail) != 0 && __lane_id() == 0) atomicOr(&flags[sok ? 1 : 0], 1u);
+  if (__ballot(fail) != 0 && __lane_id() == 0) atomicOr(slow, 1u);
 }
 
 // The array holds exactly nvals numbers and is bracketed; an empty array
 // holds nothing but whitespace (with numbers, the lanes above check the rest).
-__global__ __launch_bounds__(256) void k_xdec_check(Text t, Hier h, size_t nb,
-                                                    size_t nvals, unsigned long long* bad) {
+struct ScanTotal {
+  const uint64_t* bscan;
+  size_t nb;
+  __device__ __forceinline__ uint64_t total() const { return bscan[nb] & kCountMask; }
+};
+
+template <class Totals>
+__global__ __launch_bounds__(256) void k_xdec_check(Text t, Totals tot, size_t nvals,
+                                                    unsigned long long* bad) {
   __shared__ size_t az[2];
   __shared__ uint64_t stotal;
-  if (threadIdx.x < 64) {  // every span's count
-    const uint64_t v = hier_total(h, nb);
+  if (threadIdx.x < 64) {
+    const uint64_t v = tot.total();
     if (threadIdx.x == 0) stotal = v;
   }
   __syncthreads();
@@ -1153,78 +1063,84 @@ __global__ __launch_bounds__(256) void k_xdec_check(Text t, Hier h, size_t nb,
 
 unsigned blocks_of(size_t n, size_t per) { return (unsigned)((n + per - 1) / per); }
 
+// exclusive scan of x[0..n) in place, x[n] = total; bsum: blocks_of(n)+1 scratch
+hipError_t scan_u64(uint64_t* x, size_t n, uint64_t* bsum, LaunchCfg c) {
+  const unsigned nb = blocks_of(n, kScanBlock);
+  if (nb <= 1) {
+    AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c, x, n);
+    return hipGetLastError();
+  }
+  LaunchCfg c0 = c, c1 = c, c2 = c;
+  c0.ev_stop = nullptr;
+  c1.ev_start = c1.ev_stop = nullptr;
+  c2.ev_start = nullptr;
+  AMPH_LAUNCH(k_scan_reduce, dim3(nb), dim3(kScanBlock), c0, x, n, bsum);
+  AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c1, bsum, (size_t)nb);
+  AMPH_LAUNCH(k_scan_apply, dim3(nb), dim3(kScanBlock), c2, x, n, bsum, (size_t)nb);
+  return hipGetLastError();
+}
+
 }  // namespace
 
-size_t xenc_scratch_bytes(size_t npairs) {  // block lengths, the l1 / l2 sums, one flag word
+size_t xenc_scratch_bytes(size_t npairs) {
   const size_t nb = blocks_of(npairs, kXBlock);
-  return 8 * (nb + blocks_of(nb, kGroupSpans) + blocks_of(nb, (size_t)kGroupSpans * 64) + 1) + 8;
+  return 8 * (nb + 1) + 8 * ((size_t)blocks_of(nb, kScanBlock) + 1);
 }
 
 size_t xenc_max_bytes(size_t npairs) { return (size_t)kXEntry * npairs + 2; }
 
-// Three launches: zero the l2 sums, per-block text lengths + the hierarchy
-// (k_xenc_bsum), then k_xenc_write, which recomputes its entries' lengths
-// while converting, takes its block's offset from the hierarchy and places
-// the entries with a workgroup scan -- no per-pair length or offset array goes
-// through HBM.
+// Three passes: per-workgroup text lengths (k_xenc_bsum), a scan of those
+// (one u64 per 256 pairs), then k_xenc_write, which recomputes its entries'
+// lengths while converting and places them with a workgroup scan -- no
+// per-pair length or offset array goes through HBM.
 hipError_t launch_exchange_encode(const uint4* mag, const uint8_t* neg, size_t npairs, char* out,
                                   unsigned long long* out_len, void* scratch, const LaunchCfg& c) {
   const size_t nb = npairs ? blocks_of(npairs, kXBlock) : 0;
-  uint64_t* p = static_cast<uint64_t*>(scratch);
-  const size_t n1 = blocks_of(nb, kGroupSpans), n2 = blocks_of(nb, (size_t)kGroupSpans * 64);
-  const Hier h{p, p + nb, p + nb + n1};
+  uint64_t* bs = static_cast<uint64_t*>(scratch);
+  uint64_t* tmp = bs + nb + 1;
   LaunchCfg c0 = c, cm = c, c1 = c;
   c0.ev_stop = nullptr;
   cm.ev_start = cm.ev_stop = nullptr;
   c1.ev_start = nullptr;
-  AMPH_LAUNCH(k_hier_zero, dim3(1), dim3(256), c0, h.l2, n2 ? n2 : (size_t)1, (unsigned int*)nullptr, 0);
-  if (nb > 0)
-    AMPH_LAUNCH(k_xenc_bsum, dim3((unsigned)n1), dim3(4 * kXBlock), cm, mag, neg, npairs, nb, h);
-  AMPH_LAUNCH(k_xenc_write, dim3(nb ? (unsigned)nb : 1u), dim3(kXBlock), c1, mag, neg, npairs, h, nb, out,
-              out_len);
+  if (nb > 0) {
+    AMPH_LAUNCH(k_xenc_bsum, dim3(blocks_of(nb, 4)), dim3(4 * kXBlock), c0, mag, neg, npairs, nb, bs);
+    hipError_t e = scan_u64(bs, nb, tmp, cm);
+    if (e != hipSuccess) return e;
+  } else {
+    AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c0, bs, (size_t)0);
+  }
+  AMPH_LAUNCH(k_xenc_write, dim3(nb ? (unsigned)nb : 1u), dim3(kXBlock), c1, mag, neg, npairs, bs,
+              nb, out, out_len);
   return hipGetLastError();
 }
 
-namespace {
-struct XdecScratch {
-  Hier h;
-  unsigned int* flags;
-};
-XdecScratch xdec_layout(void* scratch, size_t nb) {
-  uint64_t* p = static_cast<uint64_t*>(scratch);
-  const size_t n1 = blocks_of(nb, kGroupSpans), n2 = blocks_of(nb, (size_t)kGroupSpans * 64);
-  XdecScratch x;
-  x.h = Hier{p, p + nb, p + nb + n1};
-  x.flags = reinterpret_cast<unsigned int*>(p + nb + n1 + n2);
-  return x;
-}
-}  // namespace
-
-size_t xdec_scratch_bytes(size_t len) {  // span counts, the l1 / l2 sums, the two flags
+size_t xdec_scratch_bytes(size_t len) {  // span counts, scan partials, the slow-path flag
   const size_t nb = blocks_of(len + 16, kDecSpan);
-  return 8 * (nb + blocks_of(nb, kGroupSpans) + blocks_of(nb, (size_t)kGroupSpans * 64) + 1);
+  return 8 * (nb + 1) + 8 * ((size_t)blocks_of(nb, kScanBlock) + 1) + 8;
 }
 
-// zero the counts and flags, the single pass, the general pass (returns at
-// once unless the single pass could not hold), the array check: four launches.
 hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, uint4* mag,
                                   uint8_t* neg, unsigned long long* bad, void* scratch,
                                   const LaunchCfg& c) {
   const size_t mis = (uintptr_t)text & 15;
   const Text t{reinterpret_cast<const uint8_t*>(text) - mis, mis, mis + len};
   const size_t nb = blocks_of(t.L ? t.L : 1, kDecSpan);
-  const XdecScratch x = xdec_layout(scratch, nb);
-  const size_t nwords = nb + blocks_of(nb, kGroupSpans) + blocks_of(nb, (size_t)kGroupSpans * 64);
   LaunchCfg c0 = c, cm = c, c1 = c;
   c0.ev_stop = nullptr;
   cm.ev_start = cm.ev_stop = nullptr;
   c1.ev_start = nullptr;
-  AMPH_LAUNCH(k_hier_zero, dim3(std::min<unsigned>(blocks_of(nwords, 256), 256u)), dim3(256), c0, x.h.l0, nwords,
-              x.flags, 2);
-  AMPH_LAUNCH(k_xdec_one, dim3((unsigned)nb), dim3(kDecBlock), cm, t, x.h, nb, 2 * npairs, mag, neg, x.flags);
-  AMPH_LAUNCH(k_xdec_slow, dim3((unsigned)std::min<size_t>(nb, kSlowGrid)), dim3(kDecBlock), cm, t, x.h, nb,
-              2 * npairs, mag, neg, bad, (const unsigned int*)x.flags);
-  AMPH_LAUNCH(k_xdec_check, dim3(1), dim3(256), c1, t, x.h, nb, 2 * npairs, bad);
+  // count, scan, compact pass, general pass, check
+  uint64_t* bscan = static_cast<uint64_t*>(scratch);
+  uint64_t* bsum = bscan + nb + 1;
+  unsigned int* slow = reinterpret_cast<unsigned int*>(bsum + blocks_of(nb, kScanBlock) + 1);
+  AMPH_LAUNCH(k_xdec_count, dim3(blocks_of(nb, kCntWaves)), dim3(64 * kCntWaves), c0, t, bscan, nb, slow);
+  hipError_t e = scan_u64(bscan, nb, bsum, cm);
+  if (e != hipSuccess) return e;
+  AMPH_LAUNCH(k_xdec_fast, dim3((unsigned)nb), dim3(kDecBlock), cm, t, bscan, nb, 2 * npairs, mag, neg,
+              slow);
+  AMPH_LAUNCH(k_xdec_slow<ScanBases>, dim3((unsigned)std::min<size_t>(nb, kSlowGrid)), dim3(kDecBlock), cm, t,
+              ScanBases{bscan, nb}, nb, 2 * npairs, mag, neg, bad, (const unsigned int*)slow);
+  AMPH_LAUNCH(k_xdec_check<ScanTotal>, dim3(1), dim3(256), c1, t, ScanTotal{bscan, nb}, 2 * npairs, bad);
   return hipGetLastError();
 }
 

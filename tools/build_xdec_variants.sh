@@ -19,11 +19,11 @@ variant() {  # name [-Dflags] sed-expression...
     $defs -DXDEC_SRC="\"$D/exchange_$name.hip\"" "$ROOT/tools/ubench/ubench_xdec2.hip" -o "$D/ubench_xdec2_$name" &
 }
 variant base
-# count pass with plain loads (text tail left in the Infinity Cache), compact pass from the end
-# the compact pass without its parse loop (window + colon listing + scan only)
-variant noparse 's/for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {/for (uint32_t idx = threadIdx.x; idx < 0u; idx += kDecBlock) {/'
-# digit run + segment checks, no base-10^8 conversion
-variant noconv 's/^  const uint32_t full = nd >> 3, rem = nd \& 7u;$/  r.v[0] = nd; r.v[1] = r.v[2] = r.v[3] = 0; return true;\n  const uint32_t full = nd >> 3, rem = nd \& 7u;/'
+# the single-read decode (published counts instead of the count pass)
+variant fused -DAMPH_XDEC_FUSED=1
+# the general pass's grid (its early exit vs its own speed)
+variant g1k -DAMPH_XDEC_SLOW_GRID=1024
+variant g16k -DAMPH_XDEC_SLOW_GRID=16384
 for v in "$@"; do :; done
 wait
 ls -la "$D"
