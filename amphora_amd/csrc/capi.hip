@@ -48,6 +48,15 @@ int hip_fail(hipError_t e, const char* what) {
     if (e_ != hipSuccess) return hip_fail(e_, #expr);   \
   } while (0)
 
+// The context's device for this thread's next HIP calls: hipSetDevice only
+// when the thread's current device differs (hipGetDevice reads thread-local
+// state; the set is what a thread's first HIP call pays for).
+hipError_t use_device(int device) {
+  int cur = -1;
+  if (hipGetDevice(&cur) == hipSuccess && cur == device) return hipSuccess;
+  return hipSetDevice(device);
+}
+
 typedef unsigned __int128 u128;
 
 u128 ld128(const uint8_t* b) {
@@ -279,7 +288,7 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
   if (words == 0) return AMPH_OK;
   constexpr int S = amph_ctx::kSlots;
   static_assert(S >= 3, "one stream per engine");
-  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(use_device(c->device));
   for (int s = 0; s < S; ++s) {
     if (!c->streams[s]) HIP_TRY(hipStreamCreateWithFlags(&c->streams[s], hipStreamNonBlocking));
     amph_ctx::Slot& sl = c->slots[s];
@@ -487,7 +496,7 @@ int run_small(amph_ctx* c, size_t words, const std::vector<HostIn>& ins, const s
               bool with_ff, int64_t* first_fail, Launch& launch, size_t bytes) {
   if (first_fail) *first_fail = -1;
   if (words == 0) return AMPH_OK;
-  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(use_device(c->device));
   hipStream_t s;
   if (int st = host_stream1(c, &s)) return st;
   Arena a;
@@ -750,7 +759,7 @@ void amph_ctx_destroy(amph_ctx* c) {
   for (amph_ctx* s : c->sub) amph_ctx_destroy(s);
   c->sub.clear();
   if (c->streams[0] || c->slots[0].dev.p || c->ff.p) {
-    (void)hipSetDevice(c->device);
+    (void)use_device(c->device);
     for (int s = 0; s < amph_ctx::kSlots; ++s) {
       if (c->streams[s]) (void)hipStreamSynchronize(c->streams[s]);
       c->slots[s].dev.release();
@@ -766,13 +775,13 @@ void amph_ctx_destroy(amph_ctx* c) {
     c->xstage.release();
   }
   if (c->small.p || c->small_ff.p) {
-    (void)hipSetDevice(c->device);
+    (void)use_device(c->device);
     if (c->streams[1]) (void)hipStreamSynchronize(c->streams[1]);
     c->small.release();
     c->small_ff.release();
   }
   if (c->xdev_done) {
-    (void)hipSetDevice(c->device);
+    (void)use_device(c->device);
     (void)hipEventSynchronize(c->xdev_done);
     (void)hipEventDestroy(c->xdev_done);
   }
@@ -800,7 +809,7 @@ int amph_recombine_verify(amph_ctx* c, const amph_odo* odos, int n, uint8_t* out
     if (int st = check_dev_odos(odos, n)) return st;
     if (int st = check_dev_words({out_secrets})) return st;
     hipStream_t s = (hipStream_t)stream;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     if (int st = reset_ff_dev(first_fail, flags, s)) return st;
     amph::OdoSet set{};
     for (int k = 0; k < 5; ++k)
@@ -836,7 +845,7 @@ int amph_mask_input(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* sec
     if (int st = check_dev_odos(odos, n)) return st;
     if (int st = check_dev_words({secrets, out_masked})) return st;
     hipStream_t s = (hipStream_t)stream;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     if (int st = reset_ff_dev(first_fail, flags, s)) return st;
     amph::OdoSet set{};
     for (int k = 0; k < 5; ++k)
@@ -891,7 +900,7 @@ int amph_recombine(amph_ctx* c, const uint8_t* const* shares, int n, size_t nbyt
     for (int j = 0; j < n; ++j)
       if (int st = check_dev_words({shares[j]})) return st;
     if (int st = check_dev_words({out})) return st;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     amph::ShareSet set{};
     for (int j = 0; j < n; ++j) set.s[j] = (const uint4*)shares[j];
     hipError_t e = amph::launch_recombine(set, n, W, (uint4*)out, c->f, cfg(c, (hipStream_t)stream, W));
@@ -917,7 +926,7 @@ int amph_verify(amph_ctx* c, const uint8_t* y, const uint8_t* r, const uint8_t* 
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({y, r, u, v, w})) return st;
     hipStream_t s = (hipStream_t)stream;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     if (int st = reset_ff_dev(first_fail, flags, s)) return st;
     hipError_t e = amph::launch_verify((const uint4*)y, (const uint4*)r, (const uint4*)u,
                                        (const uint4*)v, (const uint4*)w, words,
@@ -962,7 +971,7 @@ int amph_convert_share(amph_ctx* c, const uint8_t* masked, const uint8_t* tuples
   const W4 alpha = amph::mont_mul(w4_of(ld128(mac_key_le)), amph::r2_word(c->f), c->f);
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({masked, tuples, out})) return st;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     hipError_t e = amph::launch_convert_share((const uint4*)masked, (const uint4*)tuples, words,
                                               alpha, use_zero, (uint4*)out, c->f,
                                               cfg(c, (hipStream_t)stream, words));
@@ -989,7 +998,7 @@ int amph_odo_pre(amph_ctx* c, const uint8_t* share_data, size_t share_stride,
   const int sw = (int)(share_stride / 16);
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({share_data, masks, triples, oy, orr, ov, omag})) return st;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     hipError_t e = amph::launch_odo_pre((const uint4*)share_data, sw, (const uint4*)masks,
                                         (const uint4*)triples, words, (uint4*)oy, (uint4*)orr,
                                         (uint4*)ov, (uint4*)omag, (uint32_t*)oneg, c->f,
@@ -1020,7 +1029,7 @@ int amph_open_diffs(amph_ctx* c, const uint8_t* const* mags, const uint8_t* cons
     for (int j = 0; j < n; ++j)
       if (int st = check_dev_words({mags[j]})) return st;
     if (int st = check_dev_words({out})) return st;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     amph::SignedSet set{};
     for (int j = 0; j < n; ++j) {
       set.mag[j] = (const uint4*)mags[j];
@@ -1051,7 +1060,7 @@ int amph_odo_post(amph_ctx* c, const uint8_t* opened, const uint8_t* triples, si
   if (words && (!opened || !triples || !ow || !ou)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({opened, triples, ow, ou})) return st;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     hipError_t e = amph::launch_odo_post((const uint4*)opened, (const uint4*)triples, words,
                                          is_player0, (uint4*)ow, (uint4*)ou, c->f,
                                          cfg(c, (hipStream_t)stream, words));
@@ -1079,7 +1088,7 @@ int amph_open_post(amph_ctx* c, const uint8_t* const* mags, const uint8_t* const
     for (int j = 0; j < n; ++j)
       if (int st = check_dev_words({mags[j]})) return st;
     if (int st = check_dev_words({triples, ow, ou})) return st;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     amph::SignedSet set{};
     for (int j = 0; j < n; ++j) {
       set.mag[j] = (const uint4*)mags[j];
@@ -1113,7 +1122,7 @@ int amph_to_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, uint
   if (words && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({in, out})) return st;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     hipError_t e = amph::launch_to_gfp((const uint4*)in, words, (uint4*)out, c->f, cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_to_gfp");
   }
@@ -1131,7 +1140,7 @@ int amph_from_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, ui
   if (words && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({in, out})) return st;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     hipError_t e = amph::launch_from_gfp((const uint4*)in, words, (uint4*)out, c->f, cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_from_gfp");
   }
@@ -1149,7 +1158,7 @@ int amph_mask_words(amph_ctx* c, const uint8_t* secrets, const uint8_t* masks, s
   if (words && (!secrets || !masks || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({secrets, masks, out})) return st;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     hipError_t e = amph::launch_mask_words((const uint4*)secrets, (const uint4*)masks, words,
                                            (uint4*)out, c->f, cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_mask_words");
@@ -1173,7 +1182,7 @@ size_t b64_padding(const char* last2) {
 template <class Launch>
 int run_tail(amph_ctx* c, const void* in, size_t in_bytes, void* out, size_t out_bytes,
              bool with_bad, unsigned long long* bad_host, Launch&& launch) {
-  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(use_device(c->device));
   hipError_t e = c->tail.ensure(512);
   if (e != hipSuccess) return fail(AMPH_E_NOMEM, "tail scratch");
   if (!c->streams[0]) HIP_TRY(hipStreamCreateWithFlags(&c->streams[0], hipStreamNonBlocking));
@@ -1197,7 +1206,7 @@ int amph_base64_encode(amph_ctx* c, const uint8_t* in, size_t nbytes, char* out,
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (nbytes && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     hipError_t e = amph::launch_b64_encode(in, nbytes, out, cfg(c, (hipStream_t)stream, (nbytes + 11) / 12));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_b64_encode");
   }
@@ -1228,7 +1237,7 @@ int amph_base64_decode(amph_ctx* c, const char* in, size_t nchars, uint8_t* out,
   }
   char last2[2];
   if (flags & AMPH_F_DEVICE) {
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     if (!bad_index) return fail(AMPH_E_PARAM, "bad_index is required");
     // one 2-byte read-back decides the padding (the only synchronous step)
     HIP_TRY(read_back((hipStream_t)stream, {{last2, in + nchars - 2, 2}}));
@@ -1279,7 +1288,7 @@ int amph_base64_encode_words(amph_ctx* c, const uint8_t* words16, size_t words, 
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({words16})) return st;
     if (int st = check_dev_records(out24)) return st;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     hipError_t e = amph::launch_b64_words((const uint4*)words16, words, out24, cfg(c, (hipStream_t)stream, words));
     return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_b64_words");
   }
@@ -1299,7 +1308,7 @@ int amph_base64_decode_words(amph_ctx* c, const char* in24, size_t words, uint8_
     if (int st = check_dev_words({out16})) return st;
     if (int st = check_dev_records(in24)) return st;
     hipStream_t s = (hipStream_t)stream;
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(use_device(c->device));
     if (int st = reset_ff_dev(bad_index, flags, s)) return st;
     hipError_t e = amph::launch_b64_unwords(in24, words, (uint4*)out16, (unsigned long long*)bad_index,
                                             cfg(c, s, words));
@@ -1376,7 +1385,7 @@ int amph_exchange_encode(amph_ctx* c, const uint8_t* mag16, const uint8_t* neg, 
                          void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (!out || !out_len || (npairs && (!mag16 || !neg))) return fail(AMPH_E_PARAM, "null buffer");
-  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(use_device(c->device));
   const size_t maxb = amph::xenc_max_bytes(npairs);
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({mag16})) return st;
@@ -1446,7 +1455,7 @@ int amph_exchange_decode(amph_ctx* c, const char* text, size_t len, size_t npair
                          uint8_t* neg, int64_t* bad_index, uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
   if ((len && !text) || (npairs && (!mag16 || !neg))) return fail(AMPH_E_PARAM, "null buffer");
-  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(use_device(c->device));
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({mag16})) return st;
     hipStream_t s = (hipStream_t)stream;
@@ -1636,7 +1645,7 @@ int amph_recombine_verify_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size
   uint32_t pad;
   if (int st = wire_check(odos, n, words, &nchars, &pad)) return st;
   if (words && !out_secrets) return fail(AMPH_E_PARAM, "null output");
-  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(use_device(c->device));
   if (flags & AMPH_F_DEVICE) {
     amph::TextSet tx{};
     for (int j = 0; j < n; ++j)
@@ -1687,7 +1696,7 @@ int amph_mask_input_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size_t wor
   if (int st = wire_check(odos, n, words, &nchars, &pad)) return st;
   if (n_secrets > words) return fail(AMPH_E_LEN, "more secret words than verified input masks");
   if (n_secrets && !secrets) return fail(AMPH_E_PARAM, "null secrets");
-  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(use_device(c->device));
   if (flags & AMPH_F_DEVICE) {
     amph::TextSet tx{};
     for (int j = 0; j < n; ++j)
@@ -1739,7 +1748,7 @@ int amph_mask_input_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size_t wor
 int amph_host_register(amph_ctx* c, void* ptr, size_t bytes) {
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (!ptr || !bytes) return fail(AMPH_E_PARAM, "null or empty range");
-  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(use_device(c->device));
   HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterPortable));
   return AMPH_OK;
 }
@@ -1747,7 +1756,7 @@ int amph_host_register(amph_ctx* c, void* ptr, size_t bytes) {
 int amph_host_unregister(amph_ctx* c, void* ptr) {
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (!ptr) return fail(AMPH_E_PARAM, "null pointer");
-  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(use_device(c->device));
   HIP_TRY(hipHostUnregister(ptr));
   return AMPH_OK;
 }
@@ -1763,7 +1772,7 @@ int amph_synth_odos(amph_ctx* c, uint64_t seed, int n, size_t words, uint8_t* co
       if (words && !out_fields[k * n + j]) return fail(AMPH_E_PARAM, "null output field");
       set.f[k][j] = (uint4*)out_fields[k * n + j];
     }
-  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(use_device(c->device));
   hipError_t e = amph::launch_synth_odos(set, n, words, seed, (uint4*)out_plain_y, fault_index,
                                          noncanon_permille, c->f, cfg(c, (hipStream_t)stream, words));
   return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_synth");
@@ -1778,7 +1787,7 @@ int amph_stream_probe(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* s
   if (words && (!secrets || !out)) return fail(AMPH_E_PARAM, "null secrets/output");
   if (int st = check_dev_odos(odos, n)) return st;
   if (int st = check_dev_words({secrets, out})) return st;
-  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(use_device(c->device));
   amph::OdoSet set{};
   for (int k = 0; k < 5; ++k)
     for (int j = 0; j < n; ++j) set.f[k][j] = (const uint4*)odo_field(odos[j], k);
@@ -1790,7 +1799,7 @@ int amph_stream_probe(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* s
 int amph_synth_words(amph_ctx* c, uint64_t seed, size_t count, uint8_t* out, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (count && !out) return fail(AMPH_E_PARAM, "null output");
-  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(use_device(c->device));
   hipError_t e = amph::launch_synth_words((uint4*)out, count, seed, c->f, cfg(c, (hipStream_t)stream, count));
   return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_synth_words");
 }

@@ -17,13 +17,17 @@
 //
 // Every word of share arithmetic runs on the GPU; the host code is what a
 // JNI-bound Java host would run around it.  Usage:
-//   c1_native [words=1024] [reps=20] [shared|own] [parties=2]   -> one JSON line on stdout
-// ("shared": both parties on one context, called from both threads at once)
+//   c1_native [words=1024] [reps=20] [shared|own] [parties=2] [pool|fresh]   -> one JSON line
+// ("shared": both parties on one context, called from both threads at once;
+//  "fresh": a new thread per party per fan-out instead of persistent workers)
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
+#include <functional>
+#include <future>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -268,22 +272,80 @@ struct Party {
 };
 
 // One call per party on its own thread (AmphoraCommunicationClient's parallel
-// fan-out); the first failure is rethrown.
+// fan-out); the first failure is rethrown.  The reference fans out with
+// parallelStream, i.e. on the ForkJoin common pool, whose threads persist: so
+// each party has ONE persistent worker thread here.  (A fresh std::thread per
+// call -- `fresh` on the command line -- pays the HIP runtime's per-thread
+// setup on its first call: ~250 us per fan-out, most of a 1 k-word upload;
+// rocprofv3 of round 3: hipSetDevice 76 us on average over 664 calls.)
+class Worker {
+ public:
+  Worker() : th_([this] { loop(); }) {}
+  ~Worker() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  std::future<void> submit(std::function<void()> f) {
+    auto task = std::make_shared<std::packaged_task<void()>>(std::move(f));
+    std::future<void> fut = task->get_future();
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back([task] { (*task)(); });
+    }
+    cv_.notify_one();
+    return fut;
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  bool stop_ = false;
+  std::thread th_;
+};
+
+bool g_fresh_threads = false;
+std::vector<std::unique_ptr<Worker>> g_workers;
+
 template <class F>
 auto fanOut(std::vector<std::unique_ptr<Party>>& parties, F f) {
   using T = decltype(f(*parties[0]));
   std::vector<T> out(parties.size());
   std::vector<std::exception_ptr> err(parties.size());
-  std::vector<std::thread> th;
-  for (size_t j = 0; j < parties.size(); ++j)
-    th.emplace_back([&, j] {
-      try {
-        out[j] = f(*parties[j]);
-      } catch (...) {
-        err[j] = std::current_exception();
-      }
-    });
-  for (auto& t : th) t.join();
+  auto job = [&](size_t j) {
+    try {
+      out[j] = f(*parties[j]);
+    } catch (...) {
+      err[j] = std::current_exception();
+    }
+  };
+  if (g_fresh_threads) {
+    std::vector<std::thread> th;
+    for (size_t j = 0; j < parties.size(); ++j) th.emplace_back(job, j);
+    for (auto& t : th) t.join();
+  } else {
+    while (g_workers.size() < parties.size()) g_workers.emplace_back(new Worker());
+    std::vector<std::future<void>> done;
+    for (size_t j = 0; j < parties.size(); ++j) done.push_back(g_workers[j]->submit([&job, j] { job(j); }));
+    for (auto& d : done) d.get();
+  }
   for (auto& e : err)
     if (e) std::rethrow_exception(e);
   return out;
@@ -314,6 +376,7 @@ int main(int argc, char** argv) {
   const int reps = argc > 2 ? std::stoi(argv[2]) : 20;
   const bool shared = argc > 3 && std::string(argv[3]) == "shared";
   const int n = argc > 4 ? std::stoi(argv[4]) : 2;  // parties
+  g_fresh_threads = argc > 5 && std::string(argv[5]) == "fresh";
   const int warm = 3;
   try {
     std::mt19937_64 rng(1);
@@ -379,10 +442,11 @@ int main(int argc, char** argv) {
     }
     std::printf("{\"tool\": \"c1_native\", \"words\": %zu, \"parties\": %d, \"contexts\": %d, \"reps\": %d, "
                 "\"upload_ms_median\": %.3f, \"upload_ms_min\": %.3f, \"download_ms_median\": %.3f, "
-                "\"download_ms_min\": %.3f, \"bit_exact_round_trip\": %s, \"host\": \"C++ mirror "
-                "(include/amphora.hpp), one thread per party per call, JSON open between parties\"}\n",
+                "\"download_ms_min\": %.3f, \"bit_exact_round_trip\": %s, \"fan_out\": \"%s\", \"host\": \"C++ mirror "
+                "(include/amphora.hpp), each party on its own thread, JSON open between parties\"}\n",
                 W, n, shared ? 1 : n, reps, median(up), *std::min_element(up.begin(), up.end()), median(down),
-                *std::min_element(down.begin(), down.end()), exact ? "true" : "false");
+                *std::min_element(down.begin(), down.end()), exact ? "true" : "false",
+                g_fresh_threads ? "a new thread per party per call" : "one persistent worker thread per party");
     return exact ? 0 : 1;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "c1_native: %s\n", e.what());
