@@ -26,6 +26,8 @@ run_all() {
   step bench_c4_gloo2 300 python3 bench.py --gpus 2 --backend gloo --same-device || return
   step c1_own 120 ./tools/c1_native 1024 30 own || return
   step c1_shared 120 ./tools/c1_native 1024 30 shared || return
+  step c1_own_fresh 120 ./tools/c1_native 1024 30 own 2 fresh || return
+  step c1_own_3p 120 ./tools/c1_native 1024 30 own 3 || return
   step c1_own_4k 120 ./tools/c1_native 4096 20 own || return
   step c1_own_64k 120 ./tools/c1_native 65536 10 own || return
 }
