@@ -19,11 +19,14 @@ variant() {  # name [-Dflags] sed-expression...
     $defs -DXDEC_SRC="\"$D/exchange_$name.hip\"" "$ROOT/tools/ubench/ubench_xdec2.hip" -o "$D/ubench_xdec2_$name" &
 }
 variant base
-# the single-read decode (published counts instead of the count pass)
-variant fused -DAMPH_XDEC_FUSED=1
-# the general pass's grid (its early exit vs its own speed)
-variant g1k -DAMPH_XDEC_SLOW_GRID=1024
-variant g16k -DAMPH_XDEC_SLOW_GRID=16384
+# k_xdec_fast diagnostics (outputs wrong; read its rocprofv3 time):
+#   store  - every value stored whatever its checks say (the reference for the two below)
+#   noconf - as store, each lane parsing bytes at a lane-staggered LDS offset (13-dword
+#            stride: conflict-free ds_read_b32 banks) instead of its value's
+variant store 's/if (g < nvals \&\& fast_segment(l32, at + 1 + kWinPad, g, nvals, b0 + at + 1 - text.mis, len, fn)) {/if (g < nvals \&\& (fast_segment(l32, at + 1 + kWinPad, g, nvals, b0 + at + 1 - text.mis, len, fn) || true)) {/'
+variant noconf 's/if (g < nvals \&\& fast_segment(l32, at + 1 + kWinPad, g, nvals, b0 + at + 1 - text.mis, len, fn)) {/if (g < nvals \&\& (fast_segment(l32, (threadIdx.x * 52u + 300u) % 7900u + 16u, g, nvals, b0 + at + 1 - text.mis, len, fn) || true)) {/'
+# digit run + segment checks, no base-10^8 conversion
+variant noconv 's/^  const uint32_t full = nd >> 3, rem = nd \& 7u;$/  r.v[0] = nd; r.v[1] = r.v[2] = r.v[3] = 0; return true;\n  const uint32_t full = nd >> 3, rem = nd \& 7u;/'
 for v in "$@"; do :; done
 wait
 ls -la "$D"

@@ -30,7 +30,7 @@ __global__ void k_fill(uint4* mag, uint8_t* neg, size_t nvals, int full) {
 int main(int argc, char** argv) {
   const int R = argc > 1 ? atoi(argv[1]) : 20;
   const int full = argc > 2 ? atoi(argv[2]) : 0;  // 1: full-length magnitudes (752 MB of text)
-  const size_t npairs = (size_t)8 << 20, nvals = 2 * npairs;
+  const size_t npairs = (size_t)(argc > 3 ? atoi(argv[3]) : 8) << 20, nvals = 2 * npairs;  // argv[3]: Mi pairs
   uint4 *mag, *mag2;
   uint8_t *neg, *neg2;
   char* text;
