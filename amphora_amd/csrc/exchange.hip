@@ -1026,84 +1026,6 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64
   if (__ballot(fail) != 0 && __lane_id() == 0) atomicOr(slow, 1u);
 }
 
-// A/B only (AMPH_XDEC_PERSIST = grid size, 0 = off): k_xdec_fast as a
-// persistent grid, each workgroup striding over spans with the NEXT span's
-// window loads issued (into registers) right after the current window is in
-// LDS, so they are in flight while the current span is parsed.
-#ifndef AMPH_XDEC_PERSIST
-#define AMPH_XDEC_PERSIST 0
-#endif
-__global__ __launch_bounds__(kDecBlock) void k_xdec_fastp(Text text, const uint64_t* bscan, size_t nb,
-                                                      size_t nvals, uint4* mag, uint8_t* neg,
-                                                      unsigned int* slow) {
-  if ((bscan[nb] & ~kCountMask) != 0) return;
-  __shared__ uint4 win4[kWin / 16 + 1];
-  __shared__ uint16_t pos[kMaxStarts];
-  const int c2 = min((int)threadIdx.x + 2 * kDecBlock, kWin / 16);
-  auto interior = [&](size_t sp) {
-    const long long w = (long long)(sp * kDecSpan) - kWinPad;
-    return w >= (long long)text.mis && w + 16LL * (kWin / 16 + 1) <= (long long)text.L;
-  };
-  u32x4 v0 = {0, 0, 0, 0}, v1 = v0, v2 = v0;
-  size_t span = blockIdx.x;
-  bool have = span < nb && interior(span);
-  if (have) {
-    const u32x4* a = reinterpret_cast<const u32x4*>(text.al + (span * kDecSpan - kWinPad));
-    v0 = __builtin_nontemporal_load(a + threadIdx.x);
-    v1 = __builtin_nontemporal_load(a + threadIdx.x + kDecBlock);
-    v2 = __builtin_nontemporal_load(a + c2);
-  }
-  bool fail = false;
-  const uint32_t* l32 = reinterpret_cast<const uint32_t*>(win4);
-  const size_t len = text.L - text.mis;
-  for (; span < nb; span += gridDim.x) {
-    const size_t b0 = span * kDecSpan;
-    const long long w0 = (long long)b0 - kWinPad;
-    if (have) {
-      win4[threadIdx.x] = make_uint4(v0.x, v0.y, v0.z, v0.w);
-      win4[threadIdx.x + kDecBlock] = make_uint4(v1.x, v1.y, v1.z, v1.w);
-      if ((int)threadIdx.x + 2 * kDecBlock <= kWin / 16) win4[c2] = make_uint4(v2.x, v2.y, v2.z, v2.w);
-    } else {
-      for (int c = threadIdx.x; c < kWin / 16 + 1; c += kDecBlock) win4[c] = text.chunk(w0 + 16LL * c);
-    }
-    __syncthreads();
-    const size_t nx = span + gridDim.x;
-    have = nx < nb && interior(nx);
-    if (have) {  // the next window, in flight during this span's parse
-      const u32x4* a = reinterpret_cast<const u32x4*>(text.al + (nx * kDecSpan - kWinPad));
-      v0 = __builtin_nontemporal_load(a + threadIdx.x);
-      v1 = __builtin_nontemporal_load(a + threadIdx.x + kDecBlock);
-      v2 = __builtin_nontemporal_load(a + c2);
-    }
-    const int lo = kWinPad + kDecBytes * threadIdx.x;
-    const uint4 c0 = win4[lo / 16], c1 = win4[lo / 16 + 1];
-    const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-    uint32_t m = colons32(w);
-    uint32_t total;
-    const uint32_t first = block_excl_scan32(__popc(m), &total);
-    for (int k = (int)first; m && k < kMaxStarts; m &= m - 1, ++k)
-      pos[k] = (uint16_t)(kDecBytes * threadIdx.x + __ffs(m) - 1);
-    __syncthreads();
-    fail = fail || total > (uint32_t)kMaxStarts;
-    const uint32_t nloc = min(total, (uint32_t)kMaxStarts);
-    const uint64_t gbase = bscan[span] & kCountMask;
-    for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
-      const uint32_t at = pos[idx];
-      const uint64_t g = gbase + idx;
-      FastNum fn;
-      if (g < nvals && fast_segment(l32, at + 1 + kWinPad, g, nvals, b0 + at + 1 - text.mis, len, fn)) {
-        const size_t slot = (g & ~(uint64_t)1) + (fn.key == 'b');
-        xst16(mag + slot, make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]));
-        neg[slot] = fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0;
-      } else {
-        fail = true;
-      }
-    }
-    __syncthreads();  // the next span overwrites win4 / pos
-  }
-  if (__ballot(fail) != 0 && __lane_id() == 0) atomicOr(slow, 1u);
-}
-
 // The array holds exactly nvals numbers and is bracketed; an empty array
 // holds nothing but whitespace (with numbers, the lanes above check the rest).
 struct ScanTotal {
@@ -1214,12 +1136,8 @@ hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, u
   AMPH_LAUNCH(k_xdec_count, dim3(blocks_of(nb, kCntWaves)), dim3(64 * kCntWaves), c0, t, bscan, nb, slow);
   hipError_t e = scan_u64(bscan, nb, bsum, cm);
   if (e != hipSuccess) return e;
-  if (AMPH_XDEC_PERSIST > 0)
-    AMPH_LAUNCH(k_xdec_fastp, dim3((unsigned)std::min<size_t>(nb, AMPH_XDEC_PERSIST)), dim3(kDecBlock), cm, t,
-                bscan, nb, 2 * npairs, mag, neg, slow);
-  else
-    AMPH_LAUNCH(k_xdec_fast, dim3((unsigned)nb), dim3(kDecBlock), cm, t, bscan, nb, 2 * npairs, mag, neg,
-                slow);
+  AMPH_LAUNCH(k_xdec_fast, dim3((unsigned)nb), dim3(kDecBlock), cm, t, bscan, nb, 2 * npairs, mag, neg,
+              slow);
   AMPH_LAUNCH(k_xdec_slow<ScanBases>, dim3((unsigned)std::min<size_t>(nb, kSlowGrid)), dim3(kDecBlock), cm, t,
               ScanBases{bscan, nb}, nb, 2 * npairs, mag, neg, bad, (const unsigned int*)slow);
   AMPH_LAUNCH(k_xdec_check<ScanTotal>, dim3(1), dim3(256), c1, t, ScanTotal{bscan, nb}, 2 * npairs, bad);
