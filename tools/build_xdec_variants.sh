@@ -34,6 +34,12 @@ variant noconv 's/^  const uint32_t full = nd >> 3, rem = nd \& 7u;$/  r.v[0] = 
 variant enost 's/      xst16(reinterpret_cast<uint4\*>(dal) + u, bufv\[u\]);/      if (bufv[u].x == 0x01020304u) xst16(reinterpret_cast<uint4*>(dal) + u, bufv[u]);/'
 variant enconv 's/^    nd = to_chunks(d, cd);$/    nd = 38 + (d.x \& 1); cd[0] = d.x \& 0x1FFFFFFFu; cd[1] = d.y \& 0x1FFFFFFFu; cd[2] = d.z \& 0x1FFFFFFFu; cd[3] = d.w \& 0x1FFFFFFFu; cd[4] = 99u + (d.x \& 1) * 900u;/' 's/^    ne = to_chunks(e, ce);$/    ne = 38 + (e.x \& 1); ce[0] = e.x \& 0x1FFFFFFFu; ce[1] = e.y \& 0x1FFFFFFFu; ce[2] = e.z \& 0x1FFFFFFFu; ce[3] = e.w \& 0x1FFFFFFFu; ce[4] = 99u + (e.x \& 1) * 900u;/'
 variant enfmt 's/^    o = put_digits(o, cd, nd);$/    o += nd + (cd[0] == 7u);/' 's/^    o = put_digits(o, ce, ne);$/    o += ne + (ce[0] == 7u);/'
+# k_xenc_write formatting diagnostics (text wrong):
+#   enal8  - each whole chunk's 8 digit bytes stored at an 8-aligned LDS address (does the
+#            unaligned ds_write_b64 cost?)
+#   enpart - the leading partial chunk's predicated byte stores skipped
+variant enal8 's/      __builtin_memcpy(o + base + 1, \&w0, 4);/      char* oa = o + base + 1 - ((uintptr_t)(o + base + 1) \& 7); __builtin_memcpy(oa, \&w0, 4);/' 's/      __builtin_memcpy(o + base + 5, \&w1, 4);/      __builtin_memcpy(oa + 4, \&w1, 4);/'
+variant enpart 's/      if (base + j >= 0) o\[base + j\] = (char)dig\[j\];/      if (base + j >= 0 \&\& j > 99) o[base + j] = (char)dig[j];/'
 # (the persistent compact-pass variants p1536/p2048/p4096 need exchange.hip at commit dc51c3d)
 for v in "$@"; do :; done
 wait
