@@ -13,6 +13,9 @@
  * Pinning: GetPrimitiveArrayCritical; inside a critical region a thread may
  * make no JNI call but further Get/ReleasePrimitiveArrayCritical, so every
  * array element and length is fetched before the first array is pinned.  A
+ * refused pin (NULL, OutOfMemoryError pending) releases the others and
+ * returns.  Up to 5 x 16 + 2 element references are live at once, more than
+ * the 16 a native method is guaranteed, so EnsureLocalCapacity reserves them.  A
  * verify failure is RETURNED (the smallest failing word index); the Java side
  * builds the IntegrityVerificationException message from that word's values,
  * as SecretShareUtil.java:116-129 does.  Other failures are thrown here:
@@ -56,12 +59,18 @@ static int ref(JNIEnv* env, jbyteArray a, Pin* p) {
   return 0;
 }
 
+/* room for `count` more local references (plus the few a throw needs) */
+static int reserve(JNIEnv* env, int count) {
+  return (*env)->EnsureLocalCapacity(env, count + 4) < 0 ? -1 : 0;  /* < 0: OutOfMemoryError pending */
+}
+
 /* byte[][] fields (one per party) of k = 0..4 into pins[k * n + j] */
 static int refs_odo(JNIEnv* env, jobjectArray f[5], Pin* pins, int* n) {
   for (int k = 0; k < 5; ++k)
     if (!f[k]) return throw_arg(env, "null ODO field list");
   *n = (*env)->GetArrayLength(env, f[0]);
   if (*n < 1 || *n > MAXP) return throw_arg(env, "n_parties must be in [1, 16]");
+  if (reserve(env, 5 * *n)) return -1;
   for (int k = 0; k < 5; ++k) {
     if ((*env)->GetArrayLength(env, f[k]) != *n)
       return throw_arg(env, "The provided shares must be of the same length");
@@ -75,13 +84,10 @@ static int refs_list(JNIEnv* env, jobjectArray a, Pin* pins, int* n) {
   if (!a) return throw_arg(env, "null array list");
   *n = (*env)->GetArrayLength(env, a);
   if (*n < 1 || *n > MAXP) return throw_arg(env, "n_parties must be in [1, 16]");
+  if (reserve(env, *n)) return -1;
   for (int j = 0; j < *n; ++j)
     if (ref(env, (jbyteArray)(*env)->GetObjectArrayElement(env, a, j), &pins[j])) return -1;
   return 0;
-}
-
-static void pin_all(JNIEnv* env, Pin* pins, int count) {
-  for (int i = 0; i < count; ++i) pins[i].p = (*env)->GetPrimitiveArrayCritical(env, pins[i].ref, NULL);
 }
 
 /* outputs (written) are committed, inputs aborted (never copied back) */
@@ -89,6 +95,19 @@ static void unpin_all(JNIEnv* env, Pin* pins, int count, int first_output) {
   for (int i = count - 1; i >= 0; --i)
     if (pins[i].p)
       (*env)->ReleasePrimitiveArrayCritical(env, pins[i].ref, pins[i].p, i >= first_output ? 0 : JNI_ABORT);
+}
+
+/* -1 if the VM refused a pin (OutOfMemoryError pending): the pins taken are
+   released unwritten and nothing reaches the C ABI */
+static int pin_all(JNIEnv* env, Pin* pins, int count) {
+  for (int i = 0; i < count; ++i) {
+    pins[i].p = (*env)->GetPrimitiveArrayCritical(env, pins[i].ref, NULL);
+    if (!pins[i].p) {
+      unpin_all(env, pins, i, i);
+      return -1;
+    }
+  }
+  return 0;
 }
 
 static void ptrs_of(const Pin* pins, int count, const uint8_t** ptrs, size_t* lens) {
@@ -152,7 +171,7 @@ JNIEXPORT jlong JNICALL CLIENT(recombineVerify)(JNIEnv* env, jclass cls, jlong c
   const uint8_t* ptrs[5 * MAXP];
   size_t lens[5 * MAXP];
   int64_t fail = -1;
-  pin_all(env, pins, 5 * n + 1);
+  if (pin_all(env, pins, 5 * n + 1)) return -1;
   ptrs_of(pins, 5 * n, ptrs, lens);
   const int st = amphj_recombine_verify(CTX(ctx), n, ptrs, lens, (uint8_t*)pins[5 * n].p,
                                         (size_t)pins[5 * n].len, &fail);
@@ -173,7 +192,7 @@ JNIEXPORT jlong JNICALL CLIENT(maskInput)(JNIEnv* env, jclass cls, jlong ctx, jo
   const uint8_t* ptrs[5 * MAXP];
   size_t lens[5 * MAXP];
   int64_t fail = -1;
-  pin_all(env, pins, 5 * n + 2);
+  if (pin_all(env, pins, 5 * n + 2)) return -1;
   ptrs_of(pins, 5 * n, ptrs, lens);
   const int st = amphj_mask_input(CTX(ctx), n, ptrs, lens, (const uint8_t*)pins[5 * n].p, (size_t)pins[5 * n].len,
                                   (uint8_t*)pins[5 * n + 1].p, (size_t)pins[5 * n + 1].len, &fail);
@@ -190,7 +209,7 @@ JNIEXPORT void JNICALL CLIENT(recombine)(JNIEnv* env, jclass cls, jlong ctx, job
   if (refs_list(env, shares, pins, &n) || ref(env, out, &pins[n])) return;
   const uint8_t* ptrs[MAXP];
   size_t lens[MAXP];
-  pin_all(env, pins, n + 1);
+  if (pin_all(env, pins, n + 1)) return;
   ptrs_of(pins, n, ptrs, lens);
   const int st = amphj_recombine(CTX(ctx), n, ptrs, lens, (uint8_t*)pins[n].p, (size_t)pins[n].len);
   unpin_all(env, pins, n + 1, n);
@@ -208,7 +227,7 @@ JNIEXPORT jlong JNICALL CLIENT(verify)(JNIEnv* env, jclass cls, jlong ctx, jbyte
   const uint8_t* ptrs[5];
   size_t lens[5];
   int64_t fail = -1;
-  pin_all(env, pins, 5);
+  if (pin_all(env, pins, 5)) return -1;
   ptrs_of(pins, 5, ptrs, lens);
   const int st = amphj_verify(CTX(ctx), ptrs, lens, &fail);
   unpin_all(env, pins, 5, 5);
@@ -222,7 +241,7 @@ JNIEXPORT void JNICALL CLIENT(maskWords)(JNIEnv* env, jclass cls, jlong ctx, jby
   (void)cls;
   Pin pins[3];
   if (ref(env, secrets, &pins[0]) || ref(env, masks, &pins[1]) || ref(env, out, &pins[2])) return;
-  pin_all(env, pins, 3);
+  if (pin_all(env, pins, 3)) return;
   const int st = amphj_mask_words(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len,
                                   (const uint8_t*)pins[1].p, (size_t)pins[1].len, (uint8_t*)pins[2].p,
                                   (size_t)pins[2].len);
@@ -263,7 +282,7 @@ JNIEXPORT jlong JNICALL CLIENT(recombineVerifyB64)(JNIEnv* env, jclass cls, jlon
   const uint8_t* ptrs[5 * MAXP];
   size_t lens[5 * MAXP];
   int64_t fail = -1;
-  pin_all(env, pins, 5 * n + 1);
+  if (pin_all(env, pins, 5 * n + 1)) return -1;
   ptrs_of(pins, 5 * n, ptrs, lens);
   const int st = amphj_recombine_verify_b64(CTX(ctx), n, (const char* const*)ptrs, lens, (size_t)words,
                                             (uint8_t*)pins[5 * n].p, (size_t)pins[5 * n].len, &fail);
@@ -286,7 +305,7 @@ JNIEXPORT jlong JNICALL CLIENT(maskInputB64)(JNIEnv* env, jclass cls, jlong ctx,
   const uint8_t* ptrs[5 * MAXP];
   size_t lens[5 * MAXP];
   int64_t fail = -1;
-  pin_all(env, pins, 5 * n + 2);
+  if (pin_all(env, pins, 5 * n + 2)) return -1;
   ptrs_of(pins, 5 * n, ptrs, lens);
   const int st = amphj_mask_input_b64(CTX(ctx), n, (const char* const*)ptrs, lens, (size_t)words,
                                       (const uint8_t*)pins[5 * n].p, (size_t)pins[5 * n].len,
@@ -320,7 +339,7 @@ JNIEXPORT void JNICALL SERVICE(convertShare)(JNIEnv* env, jclass cls, jlong ctx,
   if (ref(env, masked, &pins[0]) || ref(env, tuples, &pins[1]) || ref(env, macKeyLe, &pins[2]) ||
       ref(env, out, &pins[3]))
     return;
-  pin_all(env, pins, 4);
+  if (pin_all(env, pins, 4)) return;
   const int st = amphj_convert_share(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len,
                                      (const uint8_t*)pins[1].p, (size_t)pins[1].len, (const uint8_t*)pins[2].p,
                                      (size_t)pins[2].len, useZeroInputAsData ? 1 : 0, (uint8_t*)pins[3].p,
@@ -342,7 +361,7 @@ JNIEXPORT void JNICALL SERVICE(odoPre)(JNIEnv* env, jclass cls, jlong ctx, jbyte
     throw_arg(env, "The provided shares must be of the same length");
     return;
   }
-  pin_all(env, pins, 8);
+  if (pin_all(env, pins, 8)) return;
   const int st = amphj_odo_pre(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len, stride,
                                (const uint8_t*)pins[1].p, (size_t)pins[1].len, (const uint8_t*)pins[2].p,
                                (size_t)pins[2].len, (uint8_t*)pins[3].p, (uint8_t*)pins[4].p, (uint8_t*)pins[5].p,
@@ -370,7 +389,7 @@ JNIEXPORT void JNICALL SERVICE(openPost)(JNIEnv* env, jclass cls, jlong ctx, job
   }
   const uint8_t* ptrs[2 * MAXP];
   size_t lens[2 * MAXP];
-  pin_all(env, pins, 2 * n + 3);
+  if (pin_all(env, pins, 2 * n + 3)) return;
   ptrs_of(pins, 2 * n, ptrs, lens);
   const int st = amphj_open_post(CTX(ctx), n, ptrs, lens, ptrs + n, lens + n, (const uint8_t*)pins[2 * n].p,
                                  (size_t)pins[2 * n].len, isPlayer0 ? 1 : 0, (uint8_t*)pins[2 * n + 1].p,
@@ -393,13 +412,18 @@ JNIEXPORT jbyteArray JNICALL SERVICE(exchangeEncode)(JNIEnv* env, jclass cls, jl
     return NULL;
   }
   uint64_t len = 0;
-  pin_all(env, pins, 2);
+  if (pin_all(env, pins, 2)) {
+    free(text);
+    return NULL;
+  }
   const int st = amphj_exchange_encode(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len,
                                        (const uint8_t*)pins[1].p, (size_t)pins[1].len, text, cap, &len);
   unpin_all(env, pins, 2, 2);
   jbyteArray out = NULL;
   if (st != AMPH_OK) {
     throw_status(env, st);
+  } else if (len > 0x7FFFFFFFull) {
+    throw_arg(env, "the exchange text exceeds a Java array (2^31 - 1 bytes)");
   } else {
     out = (*env)->NewByteArray(env, (jsize)len);
     if (out) (*env)->SetByteArrayRegion(env, out, 0, (jsize)len, (const jbyte*)text);
@@ -418,7 +442,7 @@ JNIEXPORT void JNICALL SERVICE(exchangeDecode)(JNIEnv* env, jclass cls, jlong ct
     throw_arg(env, "interimValues span outside the body");
     return;
   }
-  pin_all(env, pins, 3);
+  if (pin_all(env, pins, 3)) return;
   const int st = amphj_exchange_decode(CTX(ctx), (const char*)pins[0].p + off, (size_t)len, (size_t)npairs,
                                        (uint8_t*)pins[1].p, (size_t)pins[1].len, (uint8_t*)pins[2].p,
                                        (size_t)pins[2].len);

@@ -6,7 +6,9 @@
  * not layout-compatible with a JVM.  The entries are implemented by
  * jni_mock.c over plain C arrays, which also checks the JNI rule that no
  * other JNI function is called inside a Get/ReleasePrimitiveArrayCritical
- * region.  The real build (jni/Makefile) uses $JAVA_HOME/include/jni.h.
+ * region, that at most 16 local references (or what EnsureLocalCapacity
+ * reserved) are live in one native call, and lets a test make a pin fail.
+ * The real build (jni/Makefile) uses $JAVA_HOME/include/jni.h.
  */
 #ifndef JNI_MOCK_H_
 #define JNI_MOCK_H_
@@ -48,6 +50,7 @@ struct JNINativeInterface_ {
   void (*SetByteArrayRegion)(JNIEnv*, jbyteArray, jsize, jsize, const jbyte*);
   jbyteArray (*NewByteArray)(JNIEnv*, jsize);
   jstring (*NewStringUTF)(JNIEnv*, const char*);
+  jint (*EnsureLocalCapacity)(JNIEnv*, jint);
 };
 
 #endif /* JNI_MOCK_H_ */

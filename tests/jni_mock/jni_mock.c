@@ -29,6 +29,10 @@ static int g_critical;    /* open critical regions */
 static int g_violations;  /* JNI calls made inside one */
 static char g_exc_class[256];
 static char g_exc_msg[1024];
+static int g_local;          /* local references made in this native call */
+static int g_capacity = 16;  /* the JNI guarantee, or what EnsureLocalCapacity reserved */
+static int g_ref_overflows;  /* local references beyond it */
+static int g_fail_pin;       /* > 0: the g_fail_pin-th pin from now returns NULL */
 
 static struct mock_obj* obj_new(int kind, jsize len, size_t elem) {
   struct mock_obj* o = (struct mock_obj*)calloc(1, sizeof *o);
@@ -44,21 +48,30 @@ static void outside_critical(void) {
   if (g_critical) ++g_violations;
 }
 
+static void new_local(void) {
+  if (++g_local > g_capacity) ++g_ref_overflows;
+}
+
+static void pending(const char* cls, const char* msg) {
+  if (!g_exc_class[0]) {  /* the first pending exception wins, as in a JVM */
+    strncpy(g_exc_class, cls, sizeof g_exc_class - 1);
+    strncpy(g_exc_msg, msg ? msg : "", sizeof g_exc_msg - 1);
+  }
+}
+
 static jclass m_FindClass(JNIEnv* env, const char* name) {
   (void)env;
   outside_critical();
   struct mock_obj* o = obj_new(KIND_CLASS, (jsize)strlen(name) + 1, 1);
   memcpy(o->data, name, strlen(name) + 1);
+  new_local();
   return o;
 }
 
 static jint m_ThrowNew(JNIEnv* env, jclass c, const char* msg) {
   (void)env;
   outside_critical();
-  if (!g_exc_class[0]) {  /* the first pending exception wins, as in a JVM */
-    strncpy(g_exc_class, (const char*)c->data, sizeof g_exc_class - 1);
-    strncpy(g_exc_msg, msg ? msg : "", sizeof g_exc_msg - 1);
-  }
+  pending((const char*)c->data, msg);
   return 0;
 }
 
@@ -71,12 +84,17 @@ static jsize m_GetArrayLength(JNIEnv* env, jarray a) {
 static jobject m_GetObjectArrayElement(JNIEnv* env, jobjectArray a, jsize i) {
   (void)env;
   outside_critical();
+  new_local();
   return (i >= 0 && i < a->len) ? ((jobject*)a->data)[i] : NULL;
 }
 
 static void* m_GetPrimitiveArrayCritical(JNIEnv* env, jarray a, jboolean* is_copy) {
   (void)env;
   if (is_copy) *is_copy = JNI_FALSE;
+  if (g_fail_pin > 0 && --g_fail_pin == 0) {  /* as a JVM out of memory: NULL + a pending error */
+    pending("java/lang/OutOfMemoryError", "mock: pin refused");
+    return NULL;
+  }
   ++g_critical;
   ++a->pinned;
   return a->data;
@@ -112,6 +130,7 @@ static void m_SetByteArrayRegion(JNIEnv* env, jbyteArray a, jsize start, jsize l
 static jbyteArray m_NewByteArray(JNIEnv* env, jsize len) {
   (void)env;
   outside_critical();
+  new_local();
   return obj_new(KIND_BYTES, len, 1);
 }
 
@@ -121,13 +140,22 @@ static jstring m_NewStringUTF(JNIEnv* env, const char* s) {
   struct mock_obj* o = obj_new(KIND_STRING, (jsize)strlen(s), 1);
   free(o->data);
   o->data = strdup(s);
+  new_local();
   return o;
+}
+
+static jint m_EnsureLocalCapacity(JNIEnv* env, jint n) {
+  (void)env;
+  outside_critical();
+  if (g_local + n > g_capacity) g_capacity = g_local + n;
+  return 0;
 }
 
 static const struct JNINativeInterface_ g_table = {
     m_FindClass,          m_ThrowNew,          m_GetArrayLength,     m_GetObjectArrayElement,
     m_GetPrimitiveArrayCritical, m_ReleasePrimitiveArrayCritical, m_GetIntArrayRegion,
     m_GetByteArrayRegion, m_SetByteArrayRegion, m_NewByteArray,      m_NewStringUTF,
+    m_EnsureLocalCapacity,
 };
 static JNIEnv g_env = &g_table;
 
@@ -160,10 +188,16 @@ JNIEXPORT const char* mock_exception_class(void) { return g_exc_class; }
 JNIEXPORT const char* mock_exception_message(void) { return g_exc_msg; }
 JNIEXPORT int mock_violations(void) { return g_violations; }
 JNIEXPORT int mock_open_criticals(void) { return g_critical; }
+JNIEXPORT int mock_ref_overflows(void) { return g_ref_overflows; }
+JNIEXPORT void mock_fail_pin(int k) { g_fail_pin = k; }
 
 JNIEXPORT void mock_clear(void) {
   g_exc_class[0] = g_exc_msg[0] = 0;
   g_violations = 0;
+  g_local = 0;  /* a new native call */
+  g_capacity = 16;
+  g_ref_overflows = 0;
+  g_fail_pin = 0;
 }
 
 JNIEXPORT void mock_free_all(void) {

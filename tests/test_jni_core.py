@@ -151,6 +151,30 @@ def test_checks_fire_before_the_abi(J):
     assert e.exception()[0] == IAE and e.clean()
 
 
+def test_local_references_and_refused_pins(J):
+    """16 parties hold 5 x 16 element references at once: the layer reserves
+    them (EnsureLocalCapacity) instead of relying on the 16 a native method is
+    guaranteed; a pin the VM refuses releases the pins already taken, unwritten,
+    and leaves its OutOfMemoryError pending -- nothing reaches the C ABI."""
+    e = Env(J)
+    ctx = C.c_int64(0)
+    word = e.bytes(b"\0" * 32)
+    J.mock_clear()
+    lists = [e.objects([word] * 16) for _ in range(5)]
+    e.call(CLIENT + "recombineVerify", C.c_int64, ctx, *lists, e.zeros(16))
+    cls, msg = e.exception()
+    assert cls == IAE and "32 needed" in msg and e.clean()
+    assert J.mock_ref_overflows() == 0
+    for k in (1, 3, 11):  # the first, a middle and the output (5 x 2 fields + out) pin refused
+        J.mock_clear()
+        lists = [e.objects([word, word]) for _ in range(5)]
+        out = e.zeros(32)
+        J.mock_fail_pin(k)
+        assert e.call(CLIENT + "recombineVerify", C.c_int64, ctx, *lists, out) == -1
+        assert e.exception() == ("java/lang/OutOfMemoryError", "mock: pin refused") and e.clean()
+        assert J.mock_commits(out) == 0 and J.mock_ref_overflows() == 0
+
+
 # ---------------------------------------------------------------- GPU --------
 @pytest.fixture(scope="module")
 def jctx(J):
