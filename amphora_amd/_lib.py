@@ -101,6 +101,15 @@ def _load():
     L.amph_stream_probe.argtypes = [vp, vp, i32, vp, sz, vp, vp]
     L.amph_recombine_verify_b64.argtypes = [vp, vp, i32, sz, vp, i64p, i64p, u32, vp]
     L.amph_mask_input_b64.argtypes = [vp, vp, i32, sz, vp, sz, vp, vp, i64p, i64p, u32, vp]
+    L.amph_party_begin.argtypes = [vp, vp, sz, vp, vp, sz, i32, vp, vp, vp, C.POINTER(vp)]
+    L.amph_party_text_len.restype = u64
+    L.amph_party_text_len.argtypes = [vp]
+    L.amph_party_text.argtypes = [vp, vp, sz]
+    L.amph_party_partner.argtypes = [vp, i32, vp, sz, i64p]
+    L.amph_party_finish.argtypes = [vp, i32, vp, vp]
+    L.amph_party_finish_b64.argtypes = [vp, i32, C.POINTER(vp)]
+    L.amph_party_free.restype = None
+    L.amph_party_free.argtypes = [vp]
     return L
 
 
@@ -117,7 +126,9 @@ EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count",
             "amph_timing_event_elapsed_ms", "amph_base64_encode", "amph_base64_decode",
             "amph_base64_encode_words", "amph_base64_decode_words", "amph_exchange_max_chars",
             "amph_exchange_encode", "amph_exchange_decode", "amph_stream_probe",
-            "amph_recombine_verify_b64", "amph_mask_input_b64"]
+            "amph_recombine_verify_b64", "amph_mask_input_b64", "amph_party_begin", "amph_party_text_len",
+            "amph_party_text", "amph_party_partner", "amph_party_finish", "amph_party_finish_b64",
+            "amph_party_free"]
 
 
 class TimingEvent:
@@ -577,6 +588,23 @@ class Context:
         self._check(st)
         return (mag, neg) if not _is_dev(a) else (mag, neg, bad)
 
+    # -- one party's Output Delivery, device-resident between steps ------------
+    def party_begin(self, share_data, share_stride: int, masks32, triples96, n_parties: int,
+                    want_yrv: bool = True) -> "PartySession":
+        """amph_party_begin from host buffers: the tuples in, (y, r, v) out
+        (unless want_yrv is False), this party's interimValues text kept on
+        the device (PartySession.text())."""
+        sd = words_view(share_data, share_stride)
+        mk, tr = words_view(masks32, 32), words_view(triples96, 96)
+        W = sd.shape[0]
+        _need(mk.shape[0] == 2 * W, "expected %d input-mask tuples, got %d" % (2 * W, mk.shape[0]))
+        _need(tr.shape[0] == 2 * W, "expected %d multiplication triples, got %d" % (2 * W, tr.shape[0]))
+        yrv = tuple(np.empty((W, 16), np.uint8) for _ in range(3)) if want_yrv else (None, None, None)
+        h = C.c_void_p()
+        self._check(lib.amph_party_begin(self._h, _ptr(sd), share_stride, _ptr(mk), _ptr(tr), W, n_parties,
+                                         *[_ptr(x) for x in yrv], C.byref(h)))
+        return PartySession(self, h, W, n_parties, yrv)
+
     # -- synthetic device inputs (bench / tests) --------------------------------
     def synth_odos(self, seed: int, n: int, words: int, fault_index: int = -1,
                    noncanon_permille: int = 0, with_plain: bool = False):
@@ -598,3 +626,62 @@ class Context:
         stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         self._check(lib.amph_synth_words(self._h, seed, count, _ptr(out), stream))
         return out
+
+
+class PartySession:
+    """One amph_party (include/amphora.h): a party's Output Delivery with the
+    triples, diffs and ODO fields kept on the device between begin, the
+    partners' texts and finish."""
+
+    def __init__(self, ctx: Context, h, words: int, n_parties: int, yrv):
+        self.ctx, self._h, self.words, self.n = ctx, h, words, n_parties
+        self.y, self.r, self.v = yrv
+
+    def text(self) -> bytes:
+        """This party's interimValues text (the FactorPair JSON array)."""
+        n = lib.amph_party_text_len(self._h)
+        out = np.empty(max(n, 1), np.uint8)
+        Context._check(lib.amph_party_text(self._h, _ptr(out), n))
+        return out[:n].tobytes()
+
+    def partner(self, slot: int, text):
+        """A partner's interimValues text into slot 1..n-1; raises ValueError
+        on a malformed text or a pair count other than 2 * words."""
+        if isinstance(text, str):
+            text = text.encode("utf-8")
+        a = np.frombuffer(bytes(text), np.uint8)
+        bad = C.c_int64(-1)
+        st = lib.amph_party_partner(self._h, slot, _ptr(a) if a.size else None, a.size, C.byref(bad))
+        if st in (AMPH_E_PARAM, AMPH_E_LEN) and bad.value >= 0:
+            raise ValueError(lib.amph_last_error().decode())
+        Context._check(st)
+
+    def finish(self, is_player0: bool):
+        """-> (w, u) as (W, 16) words."""
+        w, u = np.empty((self.words, 16), np.uint8), np.empty((self.words, 16), np.uint8)
+        Context._check(lib.amph_party_finish(self._h, int(is_player0), _ptr(w), _ptr(u)))
+        return w, u
+
+    def finish_b64(self, is_player0: bool):
+        """-> the five ODO fields (secretShares, rShares, vShares, wShares,
+        uShares) as base64 bytes."""
+        nc = 4 * ((16 * self.words + 2) // 3)
+        outs = [np.empty(max(nc, 1), np.uint8) for _ in range(5)]
+        arr = (C.c_void_p * 5)(*[_ptr(o) for o in outs])
+        Context._check(lib.amph_party_finish_b64(self._h, int(is_player0), arr))
+        return [o[:nc].tobytes() for o in outs]
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib.amph_party_free(self._h)
+        self._h = None
+
+    def __del__(self):
+        if lib is not None:
+            self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

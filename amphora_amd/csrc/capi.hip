@@ -1805,3 +1805,233 @@ int amph_synth_words(amph_ctx* c, uint64_t seed, size_t count, uint8_t* out, voi
 }
 
 }  // extern "C"
+
+// ---- one party's Output Delivery, device-resident between steps ----------------
+// (include/amphora.h, "one party's Output Delivery with device-resident state")
+// Device memory: one allocation carved into the triples, the five ODO fields,
+// every party's diffs, this party's text and the encoder's scratch; the share
+// data and masks live in a second one released once begin has run; partner
+// texts, the decoder's scratch and the base64 output share a third, grown as
+// needed.  Every copy is a blocking hipMemcpy issued with the context's stream
+// idle (kPageableRule), so caller buffers may be pageable or page-locked.
+struct amph_party {
+  amph_ctx* c = nullptr;
+  size_t W = 0;
+  int n = 0;
+  DevBuf mem, tmp, io;
+  const uint4* triples = nullptr;
+  uint4* f5[5] = {};  // y, r, v, w, u
+  uint4* mag[AMPH_MAX_PARTIES] = {};
+  uint8_t* neg[AMPH_MAX_PARTIES] = {};
+  char* text = nullptr;
+  unsigned long long* text_len_dev = nullptr;
+  void* enc_scratch = nullptr;
+  uint64_t text_len = 0;
+  uint32_t have = 0;  // bit j: party j's diffs are on the device (bit 0 after begin)
+  bool finished = false;
+  ~amph_party() {
+    mem.release();
+    tmp.release();
+    io.release();
+  }
+};
+
+namespace {
+size_t b64_chars(size_t nbytes) { return 4 * ((nbytes + 2) / 3); }
+
+int party_check(amph_party* p) {
+  if (!p || !p->c) return fail(AMPH_E_PARAM, "null party session");
+  if (p->finished) return fail(AMPH_E_PARAM, "the party session is already finished");
+  return AMPH_OK;
+}
+
+// the summed diffs -> w, u on the device (every partner's text must be in)
+int party_open_post(amph_party* p, int is_player0, hipStream_t s) {
+  const uint32_t all = p->n >= 32 ? ~0u : ((1u << p->n) - 1u);
+  if ((p->have & all) != all) {
+    int j = 1;
+    while (j < p->n && (p->have >> j & 1u)) ++j;
+    return fail(AMPH_E_PARAM, "partner slot " + std::to_string(j) + "'s interimValues text is missing");
+  }
+  amph::SignedSet set{};
+  for (int j = 0; j < p->n; ++j) {
+    set.mag[j] = p->mag[j];
+    set.neg[j] = (const uint32_t*)p->neg[j];
+  }
+  hipError_t e = amph::launch_open_post(set, p->n, p->triples, p->W, is_player0, p->f5[3], p->f5[4], p->c->f,
+                                        cfg(p->c, s, p->W));
+  return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_open_post");
+}
+}  // namespace
+
+extern "C" {
+
+int amph_party_begin(amph_ctx* c, const uint8_t* share_data, size_t share_stride, const uint8_t* masks,
+                     const uint8_t* triples, size_t words, int n_parties, uint8_t* oy, uint8_t* orr,
+                     uint8_t* ov, amph_party** out) {
+  if (!out) return fail(AMPH_E_PARAM, "null session output");
+  *out = nullptr;
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (share_stride != 16 && share_stride != 32) return fail(AMPH_E_PARAM, "share_stride must be 16 or 32");
+  if (n_parties < 1 || n_parties > AMPH_MAX_PARTIES) return fail(AMPH_E_PARAM, "n_parties must be in [1, 16]");
+  if (words && (!share_data || !masks || !triples)) return fail(AMPH_E_PARAM, "null buffer");
+  if (!c->sub.empty()) c = c->sub[0];  // a multi-device context runs sessions on its first device
+  HIP_TRY(use_device(c->device));
+  std::lock_guard<std::mutex> g(c->mu);
+  std::unique_ptr<amph_party> p(new amph_party);
+  p->c = c;
+  p->W = words;
+  p->n = n_parties;
+  const size_t W = words, P = 2 * words;
+  const size_t sz[] = {192 * W, 16 * W, 16 * W, 16 * W, 16 * W, 16 * W,
+                       amph::xenc_max_bytes(P), 8, amph::xenc_scratch_bytes(P)};
+  size_t total = 0;
+  for (size_t b : sz) total += align256(b ? b : 16);
+  for (int j = 0; j < n_parties; ++j) total += align256(64 * W ? 64 * W : 16) + align256(4 * W ? 4 * W : 16);
+  if (p->mem.ensure(total) != hipSuccess) return fail(AMPH_E_NOMEM, "party session device memory");
+  uint8_t* cur = (uint8_t*)p->mem.p;
+  auto take = [&](size_t b) {
+    uint8_t* q = cur;
+    cur += align256(b ? b : 16);
+    return q;
+  };
+  p->triples = (const uint4*)take(sz[0]);
+  for (int k = 0; k < 5; ++k) p->f5[k] = (uint4*)take(sz[1 + k]);
+  p->text = (char*)take(sz[6]);
+  p->text_len_dev = (unsigned long long*)take(sz[7]);
+  p->enc_scratch = take(sz[8]);
+  for (int j = 0; j < n_parties; ++j) {
+    p->mag[j] = (uint4*)take(64 * W);
+    p->neg[j] = take(4 * W);
+  }
+  if (p->tmp.ensure(align256(share_stride * W + 16) + align256(64 * W + 16)) != hipSuccess)
+    return fail(AMPH_E_NOMEM, "party session staging");
+  uint8_t* dshare = (uint8_t*)p->tmp.p;
+  uint8_t* dmasks = dshare + align256(share_stride * W + 16);
+  hipStream_t s;
+  if (int st = host_stream0(c, &s)) return st;
+  HIP_TRY(hipStreamSynchronize(s));
+  if (W) {
+    HIP_TRY(hipMemcpy(dshare, share_data, share_stride * W, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dmasks, masks, 64 * W, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy((void*)p->triples, triples, 192 * W, hipMemcpyHostToDevice));
+  }
+  hipError_t e = amph::launch_odo_pre((const uint4*)dshare, (int)(share_stride / 16), (const uint4*)dmasks,
+                                      p->triples, W, p->f5[0], p->f5[1], p->f5[2], p->mag[0],
+                                      (uint32_t*)p->neg[0], c->f, cfg(c, s, W));
+  if (e != hipSuccess) return hip_fail(e, "k_odo_pre");
+  e = amph::launch_exchange_encode(p->mag[0], p->neg[0], P, p->text, p->text_len_dev, p->enc_scratch,
+                                   cfg(c, s, P));
+  if (e != hipSuccess) return hip_fail(e, "k_xenc");
+  uint64_t len = 0;
+  HIP_TRY(read_back(s, {{&len, p->text_len_dev, 8}, {oy, p->f5[0], oy ? 16 * W : 0},
+                        {orr, p->f5[1], orr ? 16 * W : 0}, {ov, p->f5[2], ov ? 16 * W : 0}}));
+  p->text_len = len;
+  p->have = 1u;
+  p->tmp.release();
+  *out = p.release();
+  return AMPH_OK;
+}
+
+uint64_t amph_party_text_len(const amph_party* p) { return p ? p->text_len : 0; }
+
+int amph_party_text(amph_party* p, char* out, size_t out_cap) {
+  if (!p || !p->c) return fail(AMPH_E_PARAM, "null party session");
+  if (!out && p->text_len) return fail(AMPH_E_PARAM, "null output");
+  if (out_cap < p->text_len)
+    return fail(AMPH_E_LEN, "output capacity " + std::to_string(out_cap) + " below the text length " +
+                                std::to_string(p->text_len));
+  amph_ctx* c = p->c;
+  HIP_TRY(use_device(c->device));
+  std::lock_guard<std::mutex> g(c->mu);
+  hipStream_t s;
+  if (int st = host_stream0(c, &s)) return st;
+  HIP_TRY(read_back(s, {{out, p->text, p->text_len}}));
+  return AMPH_OK;
+}
+
+int amph_party_partner(amph_party* p, int slot, const char* text, size_t len, int64_t* bad_index) {
+  if (bad_index) *bad_index = -1;
+  if (int st = party_check(p)) return st;
+  if (slot < 1 || slot >= p->n)
+    return fail(AMPH_E_PARAM, "partner slot must be in [1, " + std::to_string(p->n - 1) + "]");
+  if (p->have >> slot & 1u) return fail(AMPH_E_PARAM, "partner slot " + std::to_string(slot) + " already holds a text");
+  if (len && !text) return fail(AMPH_E_PARAM, "null text");
+  amph_ctx* c = p->c;
+  HIP_TRY(use_device(c->device));
+  std::lock_guard<std::mutex> g(c->mu);
+  const size_t P = 2 * p->W, sbytes = amph::xdec_scratch_bytes(len);
+  if (p->io.ensure(align256(len + 16) + 256 + align256(sbytes)) != hipSuccess)
+    return fail(AMPH_E_NOMEM, "party session text staging");
+  uint8_t* dtext = (uint8_t*)p->io.p;
+  unsigned long long* dbad = (unsigned long long*)(dtext + align256(len + 16));
+  void* scratch = dtext + align256(len + 16) + 256;
+  hipStream_t s;
+  if (int st = host_stream0(c, &s)) return st;
+  HIP_TRY(hipStreamSynchronize(s));
+  if (len) HIP_TRY(hipMemcpy(dtext, text, len, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemsetAsync(dbad, 0x7F, 8, s));
+  hipError_t e = amph::launch_exchange_decode((const char*)dtext, len, P, p->mag[slot], p->neg[slot], dbad, scratch,
+                                              cfg(c, s, len));
+  if (e != hipSuccess) return hip_fail(e, "k_xdec");
+  int64_t bad = 0;
+  HIP_TRY(read_back(s, {{&bad, dbad, 8}}));
+  if (bad != (int64_t)AMPH_NO_FAILURE) {
+    if (bad_index) *bad_index = bad;
+    if ((size_t)bad == len)
+      return fail(AMPH_E_LEN, "interimValues must hold exactly " + std::to_string(P) + " FactorPairs");
+    return fail(AMPH_E_PARAM, "Malformed FactorPair JSON at offset " + std::to_string(bad));
+  }
+  p->have |= 1u << slot;
+  return AMPH_OK;
+}
+
+int amph_party_finish(amph_party* p, int is_player0, uint8_t* ow, uint8_t* ou) {
+  if (int st = party_check(p)) return st;
+  if (p->W && (!ow || !ou)) return fail(AMPH_E_PARAM, "null output");
+  amph_ctx* c = p->c;
+  HIP_TRY(use_device(c->device));
+  std::lock_guard<std::mutex> g(c->mu);
+  hipStream_t s;
+  if (int st = host_stream0(c, &s)) return st;
+  if (int st = party_open_post(p, is_player0, s)) return st;
+  HIP_TRY(read_back(s, {{ow, p->f5[3], 16 * p->W}, {ou, p->f5[4], 16 * p->W}}));
+  p->finished = true;
+  return AMPH_OK;
+}
+
+int amph_party_finish_b64(amph_party* p, int is_player0, char* const fields_b64[5]) {
+  if (int st = party_check(p)) return st;
+  if (!fields_b64) return fail(AMPH_E_PARAM, "null field array");
+  for (int k = 0; k < 5; ++k)
+    if (p->W && !fields_b64[k]) return fail(AMPH_E_PARAM, "null field text");
+  amph_ctx* c = p->c;
+  HIP_TRY(use_device(c->device));
+  std::lock_guard<std::mutex> g(c->mu);
+  const size_t nb = 16 * p->W, nc = b64_chars(nb), stride = align256(nc + 16);
+  if (p->io.ensure(5 * stride) != hipSuccess) return fail(AMPH_E_NOMEM, "party session text staging");
+  hipStream_t s;
+  if (int st = host_stream0(c, &s)) return st;
+  if (int st = party_open_post(p, is_player0, s)) return st;
+  char* d = (char*)p->io.p;
+  for (int k = 0; k < 5 && nb; ++k) {
+    hipError_t e = amph::launch_b64_encode((const uint8_t*)p->f5[k], nb, d + k * stride, cfg(c, s, (nb + 11) / 12));
+    if (e != hipSuccess) return hip_fail(e, "k_b64_encode");
+  }
+  HIP_TRY(read_back(s, {{fields_b64[0], d, nc}, {fields_b64[1], d + stride, nc}, {fields_b64[2], d + 2 * stride, nc},
+                        {fields_b64[3], d + 3 * stride, nc}, {fields_b64[4], d + 4 * stride, nc}}));
+  p->finished = true;
+  return AMPH_OK;
+}
+
+void amph_party_free(amph_party* p) {
+  if (!p) return;
+  if (p->c) {
+    (void)use_device(p->c->device);
+    std::lock_guard<std::mutex> g(p->c->mu);
+    if (p->c->streams[0]) (void)hipStreamSynchronize(p->c->streams[0]);
+  }
+  delete p;
+}
+
+}  // extern "C"

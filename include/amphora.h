@@ -349,6 +349,44 @@ int amph_exchange_decode(amph_ctx* ctx, const char* text, size_t len, size_t npa
                          uint8_t* mag16, uint8_t* neg, int64_t* bad_index, uint32_t flags,
                          void* stream);
 
+/* ---- one party's Output Delivery with device-resident state ---------------
+ * OutputDeliveryService.computeOutputDeliveryObject (OutputDeliveryService.java:
+ * 75-286) for one request, from host buffers, with everything that is not on
+ * the wire kept in device memory between the steps:
+ *
+ *   begin    the share data, 2*words input masks and 2*words triples in (as
+ *            amph_odo_pre); y, r, v out (optional); this party's diffs encoded
+ *            as its interimValues text (amph_exchange_encode), kept on the
+ *            device -- amph_party_text_len / amph_party_text copy it out
+ *            (multiplyShares :186-200, the MultiplicationExchangeObject sent);
+ *   partner  one partner's interimValues text in (slot 1 .. n_parties-1),
+ *            decoded on the device (recombineDiffs' input, :231-272);
+ *   finish   every party's diffs summed, multiplySharedSecrets + the w/u
+ *            encoding (:274-286, :147-152), w and u out -- or, with
+ *            amph_party_finish_b64, all five ODO fields out as base64 text
+ *            (the VerifiableSecretShare body's strings).
+ *
+ * Only the texts and the ODO fields cross PCIe: the triples, the diffs and the
+ * opened values never leave the GPU (a host-path amph_odo_pre / exchange /
+ * amph_open_post sequence moves them both ways).  Results are bit-identical to
+ * that sequence.  A session belongs to one context (calls are serialised by
+ * its mutex), holds about (192 + 68 n_parties + 48) bytes per word of device
+ * memory until amph_party_free, and may be finished once.  Status semantics
+ * as the calls it replaces (amph_exchange_decode's AMPH_E_PARAM / AMPH_E_LEN
+ * with *bad_index for a malformed partner text). */
+typedef struct amph_party amph_party;
+int amph_party_begin(amph_ctx* ctx, const uint8_t* share_data, size_t share_stride,
+                     const uint8_t* mask_tuples, const uint8_t* triples, size_t words, int n_parties,
+                     uint8_t* out_y, uint8_t* out_r, uint8_t* out_v, amph_party** out);
+uint64_t amph_party_text_len(const amph_party* party);
+int amph_party_text(amph_party* party, char* out, size_t out_cap);
+int amph_party_partner(amph_party* party, int slot, const char* text, size_t len, int64_t* bad_index);
+int amph_party_finish(amph_party* party, int is_player0, uint8_t* out_w, uint8_t* out_u);
+/* fields_b64[k], k = 0..4 (secretShares, rShares, vShares, wShares, uShares):
+ * 4 * ceil(16 * words / 3) characters each, no terminator */
+int amph_party_finish_b64(amph_party* party, int is_player0, char* const fields_b64[5]);
+void amph_party_free(amph_party* party);
+
 /* ---- benchmark / test input generation (device pointers only) ---------- */
 /* Honest n-party ODOs: out_fields[k * n_parties + j] = field k (y,r,v,w,u) of
  * party j (device, words x 16 B each).  out_plain_y (optional, device) gets the

@@ -6,7 +6,9 @@ are pageable):
 
 * party Output Delivery: odo_pre -> exchange text (bytes, as a server sends
   it) -> the N-1 partners' texts decoded -> open_post -> base64 of the five
-  ODO fields;
+  ODO fields; then the same through a device-resident party session
+  (amph_party_begin / _text / _partner / _finish_b64), where only the texts
+  and the base64 fields cross PCIe;
 * client download / upload straight from the parties' base64 text
   (amph_recombine_verify_b64 / amph_mask_input_b64).
 
@@ -123,6 +125,26 @@ def party(mark):
     mark("base64_encode_x5")
 
 
+def party_session(mark):
+    """the same party through amph_party_*: only the texts and the base64 ODO
+    fields cross PCIe (y/r/v come back as base64 from finish)"""
+    ph = C.c_void_p()
+    ok(L.amph_party_begin(h, _ptr(share), 32, _ptr(masks), _ptr(triples), W, n, None, None, None, C.byref(ph)))
+    mark("begin")
+    ln = L.amph_party_text_len(ph)
+    ok(L.amph_party_text(ph, _ptr(text), cap))
+    mark("own_text")
+    for j in range(1, n):
+        ok(L.amph_party_partner(ph, j, _ptr(text), ln, C.byref(bad)))
+    mark("partners_x%d" % (n - 1))
+    ok(L.amph_party_finish_b64(ph, 0, b64_arr))
+    mark("finish_b64")
+    L.amph_party_free(ph)
+
+
+b64_arr = (C.c_void_p * 5)(*[_ptr(o) for o in b64_out])
+
+
 def download(mark):
     ok(L.amph_recombine_verify_b64(h, b64_odo_arr, n, W, _ptr(secrets_out), C.byref(ff), C.byref(bad), 0, None))
     mark("recombine_verify_b64")
@@ -135,7 +157,8 @@ def upload(mark):
 
 
 out = {"words": W, "parties": n, "memory": "host, page-locked" if a.pinned else "host, pageable",
-       "party_output_delivery": stages(party), "client_download": stages(download),
+       "party_output_delivery": stages(party), "party_output_delivery_session": stages(party_session),
+       "client_download": stages(download),
        "client_upload": stages(upload),
        "text_bytes": {"exchange": tlen.value, "odo_field_b64": int(b64_odos[0][0].size)}}
 print(json.dumps(out))
