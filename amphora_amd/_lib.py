@@ -102,6 +102,8 @@ def _load():
     L.amph_recombine_verify_b64.argtypes = [vp, vp, i32, sz, vp, i64p, i64p, u32, vp]
     L.amph_mask_input_b64.argtypes = [vp, vp, i32, sz, vp, sz, vp, vp, i64p, i64p, u32, vp]
     L.amph_party_begin.argtypes = [vp, vp, sz, vp, vp, sz, i32, vp, vp, vp, C.POINTER(vp)]
+    L.amph_party_words.restype = sz
+    L.amph_party_words.argtypes = [vp]
     L.amph_party_text_len.restype = u64
     L.amph_party_text_len.argtypes = [vp]
     L.amph_party_text.argtypes = [vp, vp, sz]
@@ -126,7 +128,7 @@ EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count",
             "amph_timing_event_elapsed_ms", "amph_base64_encode", "amph_base64_decode",
             "amph_base64_encode_words", "amph_base64_decode_words", "amph_exchange_max_chars",
             "amph_exchange_encode", "amph_exchange_decode", "amph_stream_probe",
-            "amph_recombine_verify_b64", "amph_mask_input_b64", "amph_party_begin", "amph_party_text_len",
+            "amph_recombine_verify_b64", "amph_mask_input_b64", "amph_party_begin", "amph_party_words", "amph_party_text_len",
             "amph_party_text", "amph_party_partner", "amph_party_finish", "amph_party_finish_b64",
             "amph_party_free"]
 

@@ -1933,6 +1933,8 @@ int amph_party_begin(amph_ctx* c, const uint8_t* share_data, size_t share_stride
   return AMPH_OK;
 }
 
+size_t amph_party_words(const amph_party* p) { return p ? p->W : 0; }
+
 uint64_t amph_party_text_len(const amph_party* p) { return p ? p->text_len : 0; }
 
 int amph_party_text(amph_party* p, char* out, size_t out_cap) {

@@ -26,6 +26,8 @@
  *                           + w/u encoding :147-152
  *   amph_open_post       <- recombineDiffs :231-272 + multiplySharedSecrets :274-286
  *                           + w/u encoding :147-152 (the two calls above, fused)
+ *   amph_party_*         <- computeOutputDeliveryObject :75-286 for one request with the
+ *                           triples, diffs and ODO fields device-resident between steps
  *   amph_mask_words      <- SecretShareUtil.maskInput :65-68 (canonical mask given)
  *   amph_to_gfp / amph_from_gfp <- MpSpdzIntegrationUtils.toGfp / fromGfp (call
  *                           sites: client SecretShareUtil.java:56,67; service
@@ -370,14 +372,18 @@ int amph_exchange_decode(amph_ctx* ctx, const char* text, size_t len, size_t npa
  * opened values never leave the GPU (a host-path amph_odo_pre / exchange /
  * amph_open_post sequence moves them both ways).  Results are bit-identical to
  * that sequence.  A session belongs to one context (calls are serialised by
- * its mutex), holds about (192 + 68 n_parties + 48) bytes per word of device
- * memory until amph_party_free, and may be finished once.  Status semantics
+ * its mutex), holds 456 + 68 n_parties bytes per word of device memory (the
+ * triples, five fields, every party's diffs, its own text at most) plus one
+ * partner text at a time until amph_party_free, and may be finished once.
+ * amph_party_words = the session's word count; free sessions before their
+ * context.  Status semantics
  * as the calls it replaces (amph_exchange_decode's AMPH_E_PARAM / AMPH_E_LEN
  * with *bad_index for a malformed partner text). */
 typedef struct amph_party amph_party;
 int amph_party_begin(amph_ctx* ctx, const uint8_t* share_data, size_t share_stride,
                      const uint8_t* mask_tuples, const uint8_t* triples, size_t words, int n_parties,
                      uint8_t* out_y, uint8_t* out_r, uint8_t* out_v, amph_party** out);
+size_t amph_party_words(const amph_party* party);
 uint64_t amph_party_text_len(const amph_party* party);
 int amph_party_text(amph_party* party, char* out, size_t out_cap);
 int amph_party_partner(amph_party* party, int slot, const char* text, size_t len, int64_t* bad_index);

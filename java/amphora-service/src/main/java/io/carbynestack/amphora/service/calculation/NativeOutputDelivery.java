@@ -13,7 +13,21 @@
  *
  * The signed diffs cross the open as FactorPairs of BigIntegers exactly as in
  * the reference (unreduced x - a, |x - a| < p), so partners running the Java
- * path interoperate.  Unbuildable in this image (no JDK).
+ * path interoperate.
+ *
+ * Session (the device-resident form, INTEGRATION.md section 2): the triples,
+ * every party's diffs and the ODO fields stay on the GPU between the steps and
+ * only the texts cross PCIe (72 vs 132-170 ms for 4 Mi words x 3 parties,
+ * DESIGN.md "Round 3 in brief"):
+ *
+ *   try (Session s = new Session(ctx, shareData, 32, masks, triples, nParties, false)) {
+ *     byte[] interim = s.interimValuesText();      // the JSON array of this party's FactorPairs
+ *     // ... send it inside its MultiplicationExchangeObject, receive each partner's body ...
+ *     s.partner(slot, body, off, len);             // slot 1..nParties-1, the array's span
+ *     byte[][] odoB64 = s.finishBase64(playerId == 0);  // secretShares .. uShares as base64
+ *   }
+ *
+ * Unbuildable in this image (no JDK).
  */
 package io.carbynestack.amphora.service.calculation;
 
@@ -101,6 +115,73 @@ final class NativeOutputDelivery {
     byte[][] wu = {new byte[own.y.length], new byte[own.y.length]};
     NativeShareArithmetic.openPost(ctx, mags, negs, own.triples, isPlayer0, wu[0], wu[1]);
     return wu;
+  }
+
+  /** One request's Output Delivery with device-resident state (amph_party_*). */
+  static final class Session implements AutoCloseable {
+    private long handle;
+    final int words;
+    final byte[] y; // null unless withFields
+    final byte[] r;
+    final byte[] v;
+
+    /**
+     * @param withFields fill y, r, v here (for finish()); false leaves them on the GPU for
+     *     finishBase64()
+     */
+    Session(
+        long ctx,
+        byte[] shareData,
+        int stride,
+        TupleList<InputMask<Field.Gfp>, Field.Gfp> masks,
+        TupleList<MultiplicationTriple<Field.Gfp>, Field.Gfp> triples,
+        int nParties,
+        boolean withFields) {
+      words = shareData.length / stride;
+      byte[] m = new byte[masks.size() * 2 * W16];
+      for (int i = 0; i < masks.size(); i++) put(masks.get(i).getShare(0), m, 2 * i);
+      byte[] t = new byte[triples.size() * 6 * W16];
+      for (int i = 0; i < triples.size(); i++) {
+        for (int k = 0; k < 3; k++) put(triples.get(i).getShare(k), t, 6 * i + 2 * k);
+      }
+      y = withFields ? new byte[words * W16] : null;
+      r = withFields ? new byte[words * W16] : null;
+      v = withFields ? new byte[words * W16] : null;
+      handle = NativeShareArithmetic.partyBegin(ctx, shareData, stride, m, t, nParties, y, r, v);
+    }
+
+    /** this party's MultiplicationExchangeObject.interimValues, as the JSON array Jackson writes */
+    byte[] interimValuesText() {
+      return NativeShareArithmetic.partyText(handle);
+    }
+
+    /** a partner's interimValues: body[off, off + len) is its JSON array */
+    void partner(int slot, byte[] body, int off, int len) {
+      NativeShareArithmetic.partyPartner(handle, slot, body, off, len);
+    }
+
+    /** @return {wShares, uShares} */
+    byte[][] finish(boolean isPlayer0) {
+      byte[][] wu = {new byte[words * W16], new byte[words * W16]};
+      NativeShareArithmetic.partyFinish(handle, isPlayer0, wu[0], wu[1]);
+      return wu;
+    }
+
+    /** @return the five ODO fields (secretShares, rShares, vShares, wShares, uShares) as base64 */
+    byte[][] finishBase64(boolean isPlayer0) {
+      int chars = 4 * ((words * W16 + 2) / 3);
+      byte[][] f = new byte[5][chars];
+      NativeShareArithmetic.partyFinishBase64(handle, isPlayer0, f);
+      return f;
+    }
+
+    @Override
+    public synchronized void close() {
+      if (handle != 0) {
+        NativeShareArithmetic.partyFree(handle);
+        handle = 0;
+      }
+    }
   }
 
   private static void put(Share s, byte[] out, int word) {

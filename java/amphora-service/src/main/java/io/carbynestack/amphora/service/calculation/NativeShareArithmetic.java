@@ -48,4 +48,28 @@ final class NativeShareArithmetic {
   /** body[off, off + len) = an interimValues array -> the signed diffs of npairs FactorPairs */
   static native void exchangeDecode(
       long ctx, byte[] body, int off, int len, long npairs, byte[] diffMag, byte[] diffNeg);
+
+  /*
+   * One request's Output Delivery with its triples, diffs and ODO fields kept on the GPU between
+   * the steps (amph_party_*, include/amphora.h); see NativeOutputDelivery.Session.
+   */
+
+  /** tuples in, y/r/v out (or null: finishBase64 returns them) -> a session handle */
+  static native long partyBegin(
+      long ctx, byte[] shareData, int stride, byte[] maskTuples, byte[] tripleTuples, int nParties,
+      byte[] y, byte[] r, byte[] v);
+
+  /** this party's interimValues array text */
+  static native byte[] partyText(long session);
+
+  /** partner slot 1..nParties-1: body[off, off + len) = its interimValues array */
+  static native void partyPartner(long session, int slot, byte[] body, int off, int len);
+
+  /** w, u (16 B per word) */
+  static native void partyFinish(long session, boolean isPlayer0, byte[] w, byte[] u);
+
+  /** fields[0..4] = base64 (ASCII) of secretShares, rShares, vShares, wShares, uShares */
+  static native void partyFinishBase64(long session, boolean isPlayer0, byte[][] fields);
+
+  static native void partyFree(long session);
 }

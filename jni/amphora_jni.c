@@ -449,3 +449,137 @@ JNIEXPORT void JNICALL SERVICE(exchangeDecode)(JNIEnv* env, jclass cls, jlong ct
   unpin_all(env, pins, 3, 1);
   if (st != AMPH_OK) throw_status(env, st);
 }
+
+/* ---- service: one request's Output Delivery with device-resident state ------------- */
+/* an optional array: NULL stays NULL (len 0) */
+static int ref_opt(JNIEnv* env, jbyteArray a, Pin* p) {
+  if (!a) {
+    p->ref = NULL;
+    p->len = 0;
+    p->p = NULL;
+    return 0;
+  }
+  return ref(env, a, p);
+}
+
+/* pins only the arrays that are present */
+static int pin_present(JNIEnv* env, Pin* pins, int count) {
+  for (int i = 0; i < count; ++i) {
+    if (!pins[i].ref) continue;
+    pins[i].p = (*env)->GetPrimitiveArrayCritical(env, pins[i].ref, NULL);
+    if (!pins[i].p) {
+      unpin_all(env, pins, i, i);
+      return -1;
+    }
+  }
+  return 0;
+}
+
+/* computeOutputDeliveryObject :100-139 + multiplyShares :186-200 -> a session handle
+   (y, r, v: null, or the secretShares / rShares / vShares arrays to fill) */
+JNIEXPORT jlong JNICALL SERVICE(partyBegin)(JNIEnv* env, jclass cls, jlong ctx, jbyteArray share, jint stride,
+                                            jbyteArray masks, jbyteArray triples, jint nParties, jbyteArray y,
+                                            jbyteArray r, jbyteArray v) {
+  (void)cls;
+  Pin pins[6];
+  if (ref(env, share, &pins[0]) || ref(env, masks, &pins[1]) || ref(env, triples, &pins[2]) ||
+      ref_opt(env, y, &pins[3]) || ref_opt(env, r, &pins[4]) || ref_opt(env, v, &pins[5]))
+    return 0;
+  if (pins[3].len != pins[4].len || pins[3].len != pins[5].len) {
+    throw_arg(env, "The provided shares must be of the same length");
+    return 0;
+  }
+  if (pin_present(env, pins, 6)) return 0;
+  void* session = NULL;
+  const int st = amphj_party_begin(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len, stride,
+                                   (const uint8_t*)pins[1].p, (size_t)pins[1].len, (const uint8_t*)pins[2].p,
+                                   (size_t)pins[2].len, nParties, (uint8_t*)pins[3].p, (uint8_t*)pins[4].p,
+                                   (uint8_t*)pins[5].p, (size_t)pins[3].len, &session);
+  unpin_all(env, pins, 6, 3);
+  if (st != AMPH_OK) {
+    throw_status(env, st);
+    return 0;
+  }
+  return (jlong)(intptr_t)session;
+}
+
+/* this party's MultiplicationExchangeObject.interimValues, as the JSON array text */
+JNIEXPORT jbyteArray JNICALL SERVICE(partyText)(JNIEnv* env, jclass cls, jlong session) {
+  (void)cls;
+  if (!session) return throw_arg(env, "null party session"), NULL;
+  const uint64_t len = amphj_party_text_len(CTX(session));
+  if (len > 0x7FFFFFFFull) return throw_arg(env, "the exchange text exceeds a Java array (2^31 - 1 bytes)"), NULL;
+  jbyteArray out = (*env)->NewByteArray(env, (jsize)len);
+  if (!out) return NULL; /* OutOfMemoryError pending */
+  Pin pin;
+  if (ref(env, out, &pin) || pin_all(env, &pin, 1)) return NULL;
+  const int st = amphj_party_text(CTX(session), (char*)pin.p, (size_t)pin.len);
+  unpin_all(env, &pin, 1, 0);
+  if (st != AMPH_OK) {
+    throw_status(env, st);
+    return NULL;
+  }
+  return out;
+}
+
+/* a partner's interimValues span of its received body (recombineDiffs' input :231-272) */
+JNIEXPORT void JNICALL SERVICE(partyPartner)(JNIEnv* env, jclass cls, jlong session, jint slot, jbyteArray body,
+                                             jint off, jint len) {
+  (void)cls;
+  Pin pin;
+  if (ref(env, body, &pin)) return;
+  if (off < 0 || len < 0 || (jlong)off + len > pin.len) {
+    throw_arg(env, "interimValues span outside the body");
+    return;
+  }
+  if (pin_all(env, &pin, 1)) return;
+  const int st = amphj_party_partner(CTX(session), slot, (const char*)pin.p + off, (size_t)len);
+  unpin_all(env, &pin, 1, 1);
+  if (st != AMPH_OK) throw_status(env, st);
+}
+
+/* recombineDiffs + multiplySharedSecrets + the w/u encoding :147-152, :231-286 */
+JNIEXPORT void JNICALL SERVICE(partyFinish)(JNIEnv* env, jclass cls, jlong session, jboolean isPlayer0,
+                                            jbyteArray w, jbyteArray u) {
+  (void)cls;
+  Pin pins[2];
+  if (ref(env, w, &pins[0]) || ref(env, u, &pins[1])) return;
+  if (pins[0].len != pins[1].len) {
+    throw_arg(env, "The provided shares must be of the same length");
+    return;
+  }
+  if (pin_all(env, pins, 2)) return;
+  const int st = amphj_party_finish(CTX(session), isPlayer0 ? 1 : 0, (uint8_t*)pins[0].p, (uint8_t*)pins[1].p,
+                                    (size_t)pins[0].len);
+  unpin_all(env, pins, 2, 0);
+  if (st != AMPH_OK) throw_status(env, st);
+}
+
+/* the same, with all five ODO fields returned as base64 (ASCII) in fields[0..4] */
+JNIEXPORT void JNICALL SERVICE(partyFinishBase64)(JNIEnv* env, jclass cls, jlong session, jboolean isPlayer0,
+                                                  jobjectArray fields) {
+  (void)cls;
+  Pin pins[5];
+  int n;
+  if (refs_list(env, fields, pins, &n)) return;
+  if (n != 5) {
+    throw_arg(env, "five field arrays: secretShares, rShares, vShares, wShares, uShares");
+    return;
+  }
+  if (pin_all(env, pins, 5)) return;
+  char* ptrs[5];
+  size_t lens[5];
+  for (int k = 0; k < 5; ++k) {
+    ptrs[k] = (char*)pins[k].p;
+    lens[k] = (size_t)pins[k].len;
+  }
+  const int st = amphj_party_finish_b64(CTX(session), isPlayer0 ? 1 : 0, ptrs, lens);
+  unpin_all(env, pins, 5, 0);
+  if (st != AMPH_OK) throw_status(env, st);
+}
+
+JNIEXPORT void JNICALL SERVICE(partyFree)(JNIEnv* env, jclass cls, jlong session) {
+  (void)env;
+  (void)cls;
+  amphj_party_free(CTX(session));
+}

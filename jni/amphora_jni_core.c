@@ -227,3 +227,53 @@ int amphj_exchange_decode(void* ctx, const char* text, size_t len, size_t npairs
   int64_t bad = -1;
   return abi(amph_exchange_decode((amph_ctx*)ctx, text, len, npairs, mag, neg, &bad, 0, NULL));
 }
+
+/* ---- one request's Output Delivery, device-resident between steps ---------------- */
+int amphj_party_begin(void* ctx, const uint8_t* share, size_t share_len, int stride, const uint8_t* masks,
+                      size_t masks_len, const uint8_t* triples, size_t triples_len, int n_parties, uint8_t* y,
+                      uint8_t* r, uint8_t* v, size_t out_len, void** session) {
+  *session = NULL;
+  if (stride != 16 && stride != 32) return set_msg(AMPH_E_PARAM, "share stride must be 16 or 32");
+  if (n_parties < 1 || n_parties > AMPH_MAX_PARTIES) return set_msg(AMPH_E_PARAM, "n_parties must be in [1, 16]");
+  const size_t W = share_len / (size_t)stride;
+  /* castor delivers exactly 2W input masks and 2W triples (OutputDeliveryService.java:103-107,140-146) */
+  if (room(masks_len, 2 * W * AMPH_INPUT_MASK_TUPLE_SIZE, "the input-mask stream") ||
+      room(triples_len, 2 * W * AMPH_TRIPLE_TUPLE_SIZE, "the triple stream"))
+    return AMPH_E_LEN;
+  if ((y || r || v) && (!y || !r || !v)) return set_msg(AMPH_E_PARAM, "y, r and v are all given or all null");
+  if (y && room(out_len, 16 * W, "an ODO field array")) return AMPH_E_LEN;
+  amph_party* p = NULL;
+  const int st = abi(amph_party_begin((amph_ctx*)ctx, share, (size_t)stride, masks, triples, W, n_parties, y, r, v,
+                                      &p));
+  *session = p;
+  return st;
+}
+
+uint64_t amphj_party_text_len(void* session) { return amph_party_text_len((const amph_party*)session); }
+
+int amphj_party_text(void* session, char* out, size_t out_len) {
+  if (!session) return set_msg(AMPH_E_PARAM, "null party session");
+  return abi(amph_party_text((amph_party*)session, out, out_len));
+}
+
+int amphj_party_partner(void* session, int slot, const char* text, size_t len) {
+  if (!session) return set_msg(AMPH_E_PARAM, "null party session");
+  int64_t bad = -1;
+  return abi(amph_party_partner((amph_party*)session, slot, text, len, &bad));
+}
+
+int amphj_party_finish(void* session, int is_player0, uint8_t* w, uint8_t* u, size_t out_len) {
+  if (!session) return set_msg(AMPH_E_PARAM, "null party session");
+  if (room(out_len, 16 * amph_party_words((const amph_party*)session), "an ODO field array")) return AMPH_E_LEN;
+  return abi(amph_party_finish((amph_party*)session, is_player0, w, u));
+}
+
+int amphj_party_finish_b64(void* session, int is_player0, char* const* fields, const size_t* lens) {
+  if (!session) return set_msg(AMPH_E_PARAM, "null party session");
+  const size_t nb = 16 * amph_party_words((const amph_party*)session), nc = 4 * ((nb + 2) / 3);
+  for (int k = 0; k < 5; ++k)
+    if (room(lens[k], nc, "a base64 field array")) return AMPH_E_LEN;
+  return abi(amph_party_finish_b64((amph_party*)session, is_player0, fields));
+}
+
+void amphj_party_free(void* session) { amph_party_free((amph_party*)session); }

@@ -78,6 +78,18 @@ int amphj_exchange_encode(void* ctx, const uint8_t* mag, size_t mag_len, const u
                           size_t neg_len, char* out, size_t out_cap, uint64_t* out_len);
 int amphj_exchange_decode(void* ctx, const char* text, size_t len, size_t npairs, uint8_t* mag,
                           size_t mag_len, uint8_t* neg, size_t neg_len);
+/* one request's Output Delivery with device-resident state (amph_party_*):
+ * y/r/v may be NULL (then finish_b64 returns them); texts are ASCII bytes */
+int amphj_party_begin(void* ctx, const uint8_t* share, size_t share_len, int stride, const uint8_t* masks,
+                      size_t masks_len, const uint8_t* triples, size_t triples_len, int n_parties, uint8_t* y,
+                      uint8_t* r, uint8_t* v, size_t out_len, void** session);
+uint64_t amphj_party_text_len(void* session);
+int amphj_party_text(void* session, char* out, size_t out_len);
+int amphj_party_partner(void* session, int slot, const char* text, size_t len);
+int amphj_party_finish(void* session, int is_player0, uint8_t* w, uint8_t* u, size_t out_len);
+/* fields[k] (secretShares, rShares, vShares, wShares, uShares), lens[k] bytes each */
+int amphj_party_finish_b64(void* session, int is_player0, char* const* fields, const size_t* lens);
+void amphj_party_free(void* session);
 
 #ifdef __cplusplus
 }

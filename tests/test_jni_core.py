@@ -311,3 +311,90 @@ def test_service_entry_points_two_party_output_delivery(J, jctx, F):
         opened = F.recombine_diffs([pre[j][0], pre[1 - j][0]], [pre[j][1], pre[1 - j][1]])
         ow, ou = F.odo_post(opened, triples[j], j == 0)
         assert e.read(w) == ow.tobytes() and e.read(u) == ou.tobytes()
+
+
+def test_party_session_checks_before_the_abi(J):
+    """Session entry points: argument and length checks before libamphora_hip."""
+    e = Env(J)
+    ctx = C.c_int64(0)
+    W = 10
+    share, masks, triples = e.bytes(b"\0" * 32 * W), e.bytes(b"\0" * 64 * W), e.bytes(b"\0" * 192 * W)
+    J.mock_clear()
+    assert e.call(SERVICE + "partyBegin", C.c_int64, ctx, share, C.c_int32(24), masks, triples, C.c_int32(2),
+                  None, None, None) == 0
+    assert e.exception() == (IAE, "share stride must be 16 or 32") and e.clean()
+    J.mock_clear()
+    e.call(SERVICE + "partyBegin", C.c_int64, ctx, share, C.c_int32(32), e.bytes(b"\0" * 64 * W),
+           e.bytes(b"\0" * 100), C.c_int32(2), None, None, None)
+    cls, msg = e.exception()
+    assert cls == IAE and "triple stream" in msg and e.clean()
+    J.mock_clear()  # y/r/v all or none
+    e.call(SERVICE + "partyBegin", C.c_int64, ctx, share, C.c_int32(32), masks, triples, C.c_int32(2),
+           e.zeros(16 * W), None, None)
+    assert e.exception()[0] == IAE and e.clean()
+    J.mock_clear()
+    e.call(SERVICE + "partyPartner", None, C.c_int64(0), C.c_int32(1), e.bytes(b"[]"), C.c_int32(0), C.c_int32(5))
+    assert e.exception() == (IAE, "interimValues span outside the body") and e.clean()
+    J.mock_clear()
+    e.call(SERVICE + "partyText", C.c_void_p, C.c_int64(0))
+    assert e.exception() == (IAE, "null party session") and e.clean()
+    J.mock_clear()
+    e.call(SERVICE + "partyFinishBase64", None, C.c_int64(0), C.c_uint8(1), e.objects([e.zeros(4)] * 4))
+    assert e.exception()[0] == IAE and e.clean()
+
+
+@pytest.mark.gpu
+def test_service_party_session_three_parties(J, jctx, F):
+    """A 3-party Output Delivery through the session entry points (partyBegin ->
+    partyText -> partyPartner x 2 -> partyFinish / partyFinishBase64) against
+    the oracle; inputs pinned with JNI_ABORT, outputs committed."""
+    e = Env(J)
+    ctx = C.c_int64(jctx)
+    n, W = 3, 1234
+    shares = [F.synth_words(seed=50 + j, count=2 * W).reshape(W, 32) for j in range(n)]
+    masks = [F.synth_words(seed=60 + j, count=4 * W).reshape(2 * W, 32) for j in range(n)]
+    triples = [F.synth_words(seed=70 + j, count=12 * W).reshape(2 * W, 96) for j in range(n)]
+    pre = [F.odo_pre(shares[j], 32, masks[j], triples[j]) for j in range(n)]
+    handles, texts, yrv = [], [], []
+    for j in range(n):
+        fields = (e.zeros(16 * W), e.zeros(16 * W), e.zeros(16 * W)) if j < 2 else (None, None, None)
+        share_arr = e.bytes(shares[j])
+        h = e.call(SERVICE + "partyBegin", C.c_int64, ctx, share_arr, C.c_int32(32), e.bytes(masks[j]),
+                   e.bytes(triples[j]), C.c_int32(n), *fields)
+        assert h != 0 and e.exception() is None and e.clean()
+        assert J.mock_aborts(share_arr) == 1 and J.mock_commits(share_arr) == 0
+        if j < 2:
+            assert [e.read(x) for x in fields] == [pre[j][k].tobytes() for k in range(3)]
+        txt = e.call(SERVICE + "partyText", C.c_void_p, C.c_int64(h))
+        assert e.exception() is None and e.clean()
+        handles.append(h)
+        texts.append(e.read(txt))
+        yrv.append(fields)
+    for j in range(n):
+        h = C.c_int64(handles[j])
+        for slot, k in enumerate([k for k in range(n) if k != j], start=1):
+            body = b'{"operationId":"x","playerId":%d,"interimValues":' % k + texts[k] + b"}"
+            off = body.index(b"[")
+            e.call(SERVICE + "partyPartner", None, h, C.c_int32(slot), e.bytes(body), C.c_int32(off),
+                   C.c_int32(len(texts[k])))
+            assert e.exception() is None and e.clean()
+        opened = F.recombine_diffs([pre[k][3] for k in range(n)], [pre[k][4] for k in range(n)])
+        ow, ou = F.odo_post(opened, triples[j], j == 0)
+        if j < 2:
+            w, u = e.zeros(16 * W), e.zeros(16 * W)
+            e.call(SERVICE + "partyFinish", None, h, C.c_uint8(j == 0), w, u)
+            assert e.exception() is None and e.clean()
+            assert e.read(w) == ow.tobytes() and e.read(u) == ou.tobytes()
+        else:
+            nc = 4 * ((16 * W + 2) // 3)
+            outs = [e.zeros(nc) for _ in range(5)]
+            e.call(SERVICE + "partyFinishBase64", None, h, C.c_uint8(0), e.objects(outs))
+            assert e.exception() is None and e.clean()
+            want = [base64.b64encode(x.tobytes()) for x in (pre[j][0], pre[j][1], pre[j][2], ow, ou)]
+            assert [e.read(o) for o in outs] == want
+        # a second finish is an error (the session is spent)
+        J.mock_clear()
+        e.call(SERVICE + "partyFinish", None, h, C.c_uint8(0), e.zeros(16 * W), e.zeros(16 * W))
+        assert e.exception() == (IAE, "the party session is already finished") and e.clean()
+        J.mock_clear()
+        e.call(SERVICE + "partyFree", None, h)
