@@ -84,7 +84,7 @@ class AmphoraParty:
         self.mac_key = mac_key
         self._castor = lambda rid, ttype, count: tuple_source(player_id, rid, ttype, count)
         self.odo_service = OutputDeliveryService(self.ctx, player_id, self._castor, hub.exchange,
-                                                 exchange_format)
+                                                 exchange_format, n_parties=hub.n)
         self.share_util = ServiceSecretShareUtil(self.ctx)
         self.input_mask_store: Dict[uuid.UUID, object] = {}
         self.secrets: Dict[uuid.UUID, SecretShare] = {}

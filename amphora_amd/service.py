@@ -109,18 +109,25 @@ class OutputDeliveryService:
     exchange_format="json": the exchange carries the MultiplicationExchangeObject
     as its /inter-vcp/open JSON body (bytes in, partners' bodies out), coded on
     the GPU (amph_exchange_*) -- no per-value Python objects.
+    exchange_format="session": the same JSON bodies, with the request run as a
+    device-resident party session (amph_party_*): the triples and every party's
+    diffs stay on the GPU between the open's two halves (needs n_parties).
     """
 
     def __init__(self, ctx: _lib.Context, player_id: int,
                  tuple_source: Callable[[uuid.UUID, str, int], bytes],
-                 exchange: Callable, exchange_format: str = "objects"):
-        if exchange_format not in ("objects", "json"):
-            raise ValueError("exchange_format must be 'objects' or 'json'")
+                 exchange: Callable, exchange_format: str = "objects", n_parties: int = None):
+        if exchange_format not in ("objects", "json", "session"):
+            raise ValueError("exchange_format must be 'objects', 'json' or 'session'")
+        if exchange_format == "session" and not n_parties:
+            raise ValueError("exchange_format='session' needs n_parties")
         self._ctx = ctx
         self.player_id = player_id
         self._tuples = tuple_source
         self._exchange = exchange
         self._json = exchange_format == "json"
+        self._session = exchange_format == "session"
+        self.n_parties = n_parties
         self.last_exchange_object = None
 
     def _download(self, request_id, tuple_type, count):
@@ -154,6 +161,8 @@ class OutputDeliveryService:
         masks = self._download(request_id, INPUT_MASK_GFP, 2 * W)
         op_id = name_uuid_from_bytes(("%s_%d" % (request_id, 2 * W)).encode())  # :140-141
         triples = self._download(op_id, MULTIPLICATION_TRIPLE_GFP, 2 * W)
+        if self._session:
+            return self._compute_session(share_words, stride, masks, triples, op_id)
         y, r, v, mag, neg = self._ctx.odo_pre(share_words, stride, masks, triples)
         mags, negs = [mag], [neg]
         if self._json:
@@ -187,6 +196,29 @@ class OutputDeliveryService:
         # encoding (:147-152), one launch: the opened values stay on chip
         w, u = self._ctx.open_post(mags, negs, triples, self.player_id == 0)
         return OutputDeliveryObject(y.tobytes(), r.tobytes(), v.tobytes(), w.tobytes(), u.tobytes())
+
+    def _compute_session(self, share_words, stride, masks, triples, op_id):
+        """_compute with the tuples, diffs and ODO fields device-resident
+        (amph_party_begin -> the own body -> each partner's interimValues ->
+        amph_party_finish); same results, bit for bit."""
+        from . import wire
+        with self._ctx.party_begin(share_words, stride, masks, triples, self.n_parties) as s:
+            own = wire.exchange_body(op_id, self.player_id, s.text())
+            self.last_exchange_object = own
+            try:
+                partners = self._exchange(own)
+                if len(partners) != self.n_parties - 1:
+                    raise ValueError("%d partner bodies, %d expected" % (len(partners), self.n_parties - 1))
+                for slot, body in enumerate(partners, start=1):
+                    body = bytes(body)
+                    p_op, _, lb, rb = wire.exchange_span(body)
+                    if p_op != op_id:
+                        raise ValueError("operation id %s != %s" % (p_op, op_id))
+                    s.partner(slot, body[lb:rb + 1])
+            except Exception as e:
+                raise AmphoraServiceException("Failed to open values for operation #%s" % op_id) from e
+            w, u = s.finish(self.player_id == 0)
+            return OutputDeliveryObject(s.y.tobytes(), s.r.tobytes(), s.v.tobytes(), w.tobytes(), u.tobytes())
 
     def get_input_masks_as_output_delivery_object(self, request_id: uuid.UUID, count: int):
         """InputMaskCachingService.getInputMasksAsOutputDeliveryObject :77-99:

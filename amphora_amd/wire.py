@@ -304,8 +304,20 @@ def exchange_to_json(ctx: _lib.Context, operation_id: uuid.UUID, player_id: int,
     if not isinstance(arr, bytes):  # device tensors -> host bytes
         out, n = arr
         arr = out[: int(n.item())].cpu().numpy().tobytes()
+    return exchange_body(operation_id, player_id, arr)
+
+
+def exchange_body(operation_id: uuid.UUID, player_id: int, interim_values: bytes) -> bytes:
+    """The MultiplicationExchangeObject JSON around an interimValues array text
+    (as amph_exchange_encode / amph_party_text write it)."""
     head = '{"operationId":"%s","playerId":%d,"interimValues":' % (operation_id, int(player_id))
-    return head.encode() + arr + b"}"
+    return head.encode() + bytes(interim_values) + b"}"
+
+
+def exchange_span(text) -> Tuple[uuid.UUID, int, int, int]:
+    """(operationId, playerId, lb, rb): text[lb:rb + 1] is the interimValues array."""
+    text = text.encode() if isinstance(text, str) else bytes(text)
+    return _exchange_split(text)
 
 
 def _exchange_split(text: bytes):

@@ -34,7 +34,8 @@ def _cluster(n, seed, exchange_format="json", transport="objects"):
                                                (2, 1, "json", "objects"), (2, 1000, "objects", "objects"),
                                                (3, 257, "objects", "objects"), (2, 1000, "json", "json"),
                                                (3, 769, "json", "json"), (2, 1, "json", "json"),
-                                               (4, 2, "objects", "json")])
+                                               (4, 2, "objects", "json"), (2, 1000, "session", "objects"),
+                                               (3, 769, "session", "json"), (2, 1, "session", "json")])
 def test_upload_download_roundtrip(n, W, fmt, transport):
     """fmt: the inter-VCP open carries MultiplicationExchangeObject JSON bodies
     (GPU-coded) or in-memory FactorPair lists.  transport="json": the
@@ -58,11 +59,30 @@ def test_upload_download_roundtrip(n, W, fmt, transport):
     odo_req = O.odo_request_id(sid)
     assert any(c[1] == odo_req for c in castor.calls)
     assert any(c[1] == O.operation_id(odo_req, 2 * W) for c in castor.calls)
-    if fmt == "json":  # the last open each party sent is a well-formed body
+    if fmt in ("json", "session"):  # the last open each party sent is a well-formed body
         import json
         body = json.loads(parties[0].odo_service.last_exchange_object)
         assert list(body) == ["operationId", "playerId", "interimValues"]
         assert len(body["interimValues"]) == 2 * W and body["playerId"] == 0
+    client.close()
+
+
+def test_session_and_per_call_parties_interoperate():
+    """A party running its requests as device-resident sessions and one running
+    the per-call path send each other the same JSON bodies."""
+    import amphora_amd as A
+    from amphora_amd.loopback import AmphoraParty, ExchangeHub, LoopbackAmphoraClient
+    rng = random.Random(77)
+    keys = [rng.randrange(P) for _ in range(3)]
+    castor = FakeCastor(P, R, RINV, keys, 77)
+    hub = ExchangeHub(3)
+    parties = [AmphoraParty(j, P, R, RINV, keys[j], castor, hub, exchange_format=fmt)
+               for j, fmt in enumerate(["session", "json", "session"])]
+    client = LoopbackAmphoraClient(parties, P, R, RINV, transport="json")
+    data = [rng.randrange(P) for _ in range(333)]
+    sid = client.create_secret(A.Secret.of([], data))
+    assert client.get_secret(sid).data == data
+    assert parties[0].odo_service.last_exchange_object.startswith(b'{"operationId":')
     client.close()
 
 
