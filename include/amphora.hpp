@@ -379,6 +379,46 @@ inline std::vector<std::string> maskSecretText(const SecretShareUtil& util, cons
 
 namespace service {
 
+// One request's Output Delivery with the triples, diffs and ODO fields kept on
+// the GPU between the steps (amph_party_*): begin -> text() -> partner(slot,
+// ...) for every partner -> finish().
+class PartySession {
+ public:
+  PartySession(const Context& ctx, const Bytes& shareData, size_t stride, const Bytes& maskTuples,
+               const Bytes& triples, int nParties)
+      : words_(shareData.size() / stride), y_(16 * words_), r_(16 * words_), v_(16 * words_) {
+    check(amph_party_begin(ctx.get(), shareData.data(), stride, maskTuples.data(), triples.data(), words_,
+                           nParties, y_.data(), r_.data(), v_.data(), &p_));
+  }
+  PartySession(const PartySession&) = delete;
+  PartySession& operator=(const PartySession&) = delete;
+  ~PartySession() { amph_party_free(p_); }
+
+  // this party's interimValues array (the FactorPair JSON Jackson writes)
+  std::string text() const {
+    std::string t(amph_party_text_len(p_), '\0');
+    check(amph_party_text(p_, &t[0], t.size()));
+    return t;
+  }
+  // a partner's interimValues array; IllegalArgumentException if malformed
+  void partner(int slot, const char* text, size_t len) {
+    int64_t bad = -1;
+    const int st = amph_party_partner(p_, slot, text, len, &bad);
+    if ((st == AMPH_E_PARAM || st == AMPH_E_LEN) && bad >= 0) throw IllegalArgumentException(amph_last_error());
+    check(st);
+  }
+  OutputDeliveryObject finish(bool isPlayer0) {
+    Bytes w(16 * words_), u(16 * words_);
+    check(amph_party_finish(p_, isPlayer0, w.data(), u.data()));
+    return OutputDeliveryObject(std::move(y_), std::move(r_), std::move(v_), std::move(w), std::move(u));
+  }
+
+ private:
+  size_t words_;
+  Bytes y_, r_, v_;
+  amph_party* p_ = nullptr;
+};
+
 class SecretShareUtil {
  public:
   explicit SecretShareUtil(const Context& ctx) : ctx_(ctx) {}
@@ -478,6 +518,8 @@ inline Bytes base64Decode(const Context& ctx, const std::string& text) {
   return out;
 }
 
+inline std::string exchangeBody(const std::string& operationId, int playerId, const std::string& interimValues);
+
 // Signed Beaver diffs in amph_odo_pre's layout: 2 values per pair.
 struct Diffs {
   Bytes mag;  // 32 B per pair (d, e magnitudes, LE16)
@@ -494,13 +536,17 @@ inline std::string exchangeToJson(const Context& ctx, const std::string& operati
   check(amph_exchange_encode(ctx.get(), d.mag.data(), d.neg.data(), d.pairs(), &arr[0], arr.size(), &n,
                              0, nullptr));
   arr.resize(n);
-  return "{\"operationId\":\"" + operationId + "\",\"playerId\":" + std::to_string(playerId) +
-         ",\"interimValues\":" + arr + "}";
+  return exchangeBody(operationId, playerId, arr);
 }
 
-// JSON body -> (operationId, diffs); the interimValues array is parsed on the GPU.
-inline std::pair<std::string, Diffs> exchangeFromJson(const Context& ctx, const std::string& body,
-                                                      size_t pairs) {
+// A MultiplicationExchangeObject JSON body: its operationId and the span
+// [lb, rb] of its interimValues array.
+struct ExchangeSpan {
+  std::string operationId;
+  size_t lb, rb;
+};
+
+inline ExchangeSpan exchangeSpan(const std::string& body) {
   const size_t k = body.find("\"interimValues\"");
   const size_t lb = k == std::string::npos ? k : body.find('[', k);
   const size_t rb = body.rfind(']');
@@ -514,13 +560,25 @@ inline std::pair<std::string, Diffs> exchangeFromJson(const Context& ctx, const 
     if (q1 != std::string::npos) op = body.substr(q0 + 1, q1 - q0 - 1);
   }
   if (op.empty()) throw IllegalArgumentException("operationId is marked non-null but is null");
+  return {op, lb, rb};
+}
+
+inline std::string exchangeBody(const std::string& operationId, int playerId, const std::string& interimValues) {
+  return "{\"operationId\":\"" + operationId + "\",\"playerId\":" + std::to_string(playerId) +
+         ",\"interimValues\":" + interimValues + "}";
+}
+
+// JSON body -> (operationId, diffs); the interimValues array is parsed on the GPU.
+inline std::pair<std::string, Diffs> exchangeFromJson(const Context& ctx, const std::string& body,
+                                                      size_t pairs) {
+  const ExchangeSpan sp = exchangeSpan(body);
   Diffs d{Bytes(32 * pairs), Bytes(2 * pairs)};
   int64_t bad = -1;
-  const int st = amph_exchange_decode(ctx.get(), body.data() + lb, rb + 1 - lb, pairs, d.mag.data(),
+  const int st = amph_exchange_decode(ctx.get(), body.data() + sp.lb, sp.rb + 1 - sp.lb, pairs, d.mag.data(),
                                       d.neg.data(), &bad, 0, nullptr);
   if (st == AMPH_E_PARAM || st == AMPH_E_LEN) throw IllegalArgumentException(amph_last_error());
   check(st);
-  return {op, std::move(d)};
+  return {sp.operationId, std::move(d)};
 }
 
 }  // namespace wire
@@ -536,8 +594,12 @@ class OutputDeliveryService {
   using TupleSource = std::function<Bytes(const std::string&, const std::string&, size_t)>;
   using Exchange = std::function<std::vector<std::string>(const std::string&)>;
 
-  OutputDeliveryService(const Context& ctx, int playerId, TupleSource tuples, Exchange exchange)
-      : ctx_(ctx), playerId_(playerId), tuples_(std::move(tuples)), exchange_(std::move(exchange)) {}
+  // sessionParties > 0: run each request as a PartySession of that many parties
+  // (same bodies and results; the triples and diffs stay on the GPU)
+  OutputDeliveryService(const Context& ctx, int playerId, TupleSource tuples, Exchange exchange,
+                        int sessionParties = 0)
+      : ctx_(ctx), playerId_(playerId), tuples_(std::move(tuples)), exchange_(std::move(exchange)),
+        sessionParties_(sessionParties) {}
 
   // shareData: SecretShare.data (stride 32, MACs stripped) or raw words (stride 16)
   OutputDeliveryObject computeOutputDeliveryObject(const Bytes& shareData, size_t stride,
@@ -546,6 +608,7 @@ class OutputDeliveryService {
     const Bytes masks = download(requestId, "INPUT_MASK_GFP", 2 * W, 32);
     const std::string op = nameUUIDFromBytes(requestId + "_" + std::to_string(2 * W));  // :140-141
     const Bytes triples = download(op, "MULTIPLICATION_TRIPLE_GFP", 2 * W, 96);
+    if (sessionParties_ > 0) return computeInSession(shareData, stride, masks, triples, op);
     Bytes y(16 * W), r(16 * W), v(16 * W);
     wire::Diffs own{Bytes(64 * W), Bytes(4 * W)};
     check(amph_odo_pre(ctx_.get(), shareData.data(), stride, masks.data(), triples.data(), W, y.data(),
@@ -575,6 +638,25 @@ class OutputDeliveryService {
   const std::string& lastExchangeObject() const { return lastExchange_; }
 
  private:
+  OutputDeliveryObject computeInSession(const Bytes& shareData, size_t stride, const Bytes& masks,
+                                        const Bytes& triples, const std::string& op) {
+    PartySession s(ctx_, shareData, stride, masks, triples, sessionParties_);
+    lastExchange_ = wire::exchangeBody(op, playerId_, s.text());
+    try {
+      const std::vector<std::string> bodies = exchange_(lastExchange_);
+      if ((int)bodies.size() != sessionParties_ - 1) throw IllegalArgumentException("partner count mismatch");
+      int slot = 1;
+      for (const std::string& body : bodies) {
+        const wire::ExchangeSpan sp = wire::exchangeSpan(body);
+        if (sp.operationId != op) throw IllegalArgumentException("operation id mismatch");
+        s.partner(slot++, body.data() + sp.lb, sp.rb + 1 - sp.lb);
+      }
+    } catch (const std::exception&) {
+      std::throw_with_nested(AmphoraServiceException("Failed to open values for operation #" + op));
+    }
+    return s.finish(playerId_ == 0);
+  }
+
   Bytes download(const std::string& id, const char* type, size_t count, size_t width) {
     Bytes b;
     try {
@@ -591,6 +673,7 @@ class OutputDeliveryService {
   int playerId_;
   TupleSource tuples_;
   Exchange exchange_;
+  int sessionParties_;
   std::string lastExchange_;
 };
 

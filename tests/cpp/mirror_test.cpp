@@ -71,23 +71,45 @@ static void kat2_service(const Context& c) {
                           "[{\"a\":10,\"b\":25},{\"a\":39,\"b\":24},{\"a\":1,\"b\":148},{\"a\":294,\"b\":377}]}";
   const std::string partner = "{\"operationId\":\"" + op + "\",\"playerId\":1,\"interimValues\":"
                               "[{\"a\":4,\"b\":63},{\"a\":175,\"b\":136},{\"a\":5,\"b\":106},{\"a\":2,\"b\":27}]}";
-  bool ownOk = false;
-  service::OutputDeliveryService svc(
-      c, 0,
-      [&](const std::string& id, const std::string& type, size_t count) {
-        EXPECT(count == 4);
-        if (type == "INPUT_MASK_GFP") { EXPECT(id == req); return maskTuples; }
-        EXPECT(type == "MULTIPLICATION_TRIPLE_GFP" && id == op);
-        return triples;
-      },
-      [&](const std::string& body) {
-        ownOk = body == own;
-        return std::vector<std::string>{partner};
-      });
-  OutputDeliveryObject odo = svc.computeOutputDeliveryObject(share, 32, req);
-  EXPECT(ownOk);
-  EXPECT(odo == OutputDeliveryObject(c.toGfp(secrets), c.toGfp({87, 412}), c.toGfp({111, 313}),
-                                     c.toGfp({12859, 95134}), c.toGfp({91763, 138232})));
+  for (int sessionParties : {0, 2}) {  // per-call path, then as a device-resident party session
+    bool ownOk = false;
+    service::OutputDeliveryService svc(
+        c, 0,
+        [&](const std::string& id, const std::string& type, size_t count) {
+          EXPECT(count == 4);
+          if (type == "INPUT_MASK_GFP") { EXPECT(id == req); return maskTuples; }
+          EXPECT(type == "MULTIPLICATION_TRIPLE_GFP" && id == op);
+          return triples;
+        },
+        [&](const std::string& body) {
+          ownOk = body == own;
+          return std::vector<std::string>{partner};
+        },
+        sessionParties);
+    OutputDeliveryObject odo = svc.computeOutputDeliveryObject(share, 32, req);
+    EXPECT(ownOk);
+    EXPECT(odo == OutputDeliveryObject(c.toGfp(secrets), c.toGfp({87, 412}), c.toGfp({111, 313}),
+                                       c.toGfp({12859, 95134}), c.toGfp({91763, 138232})));
+  }
+  {  // a malformed partner body in a session: the reference's open failure, the cause nested
+    service::OutputDeliveryService svc(
+        c, 0, [&](const std::string&, const std::string& type, size_t) {
+          return type == "INPUT_MASK_GFP" ? maskTuples : triples;
+        },
+        [&](const std::string&) {
+          std::string bad = partner;
+          bad[bad.find("175")] = 'x';
+          return std::vector<std::string>{bad};
+        },
+        2);
+    bool threw = false;
+    try {
+      svc.computeOutputDeliveryObject(share, 32, req);
+    } catch (const AmphoraServiceException& e) {
+      threw = std::string(e.what()) == "Failed to open values for operation #" + op;
+    }
+    EXPECT(threw);
+  }
   bool threw = false;
   service::OutputDeliveryService broken(
       c, 0, [&](const std::string&, const std::string&, size_t) -> Bytes { throw std::runtime_error("x"); },
