@@ -262,6 +262,21 @@ int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
                 const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
                 Launch& launch, size_t ff_scale);
 
+// Batch size of a host call: at most ctx->batch_words, and small enough that
+// the call has about 8 batches -- so copies in, kernels and copies out of
+// consecutive batches overlap -- but not below 32 MiB of traffic per batch
+// (each batch costs a few events and copy launches).  A 4 Mi-word call at 3
+// parties used to be ONE batch, every stage back to back: pageable odo_pre
+// 43.6 -> 25.7 ms, open_post 48.0 -> 32.8, mask_input 30.8 -> 22.5 with
+// 512 Ki-word batches (tools/host_rate_probe.py, profiles/r03_host_batches.jsonl);
+// C5's 32 Mi-word calls keep their 4 Mi-word batches.
+size_t batch_for(const amph_ctx* c, size_t words, size_t bytes_per_word) {
+  constexpr size_t kMinBatchBytes = (size_t)32 << 20;
+  const size_t floor_words = std::max<size_t>(1, kMinBatchBytes / std::max<size_t>(1, bytes_per_word));
+  const size_t eighth = (words + 7) / 8;
+  return std::max<size_t>(1, std::min({words, c->batch_words, std::max(eighth, floor_words)}));
+}
+
 // Streams `words` through the device in batches of ctx->batch_words, one
 // HIP stream per engine: streams[0] carries every HtoD copy in batch order,
 // streams[1] the kernels, streams[2] every DtoH copy.  kSlots device slots
@@ -299,7 +314,10 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
   }
   hipStream_t s_in = c->streams[0], s_k = c->streams[1], s_out = c->streams[2];
   if (!c->pool) c->pool.reset(new amph::CopyPool(host_threads() - 1));
-  const size_t bw = std::min(words, c->batch_words);
+  size_t bpw = 0;
+  for (const HostIn& x : ins) bpw += x.bytes_per_word;
+  for (const HostOut& x : outs) bpw += x.bytes_per_word;
+  const size_t bw = batch_for(c, words, bpw);
   const size_t nb = (words + bw - 1) / bw;
   std::vector<char> in_pinned(ins.size()), out_pinned(outs.size());
   size_t dev_bytes = 0, hin_bytes = 0, hout_bytes = 0;

@@ -128,7 +128,9 @@ void amph_ctx_destroy(amph_ctx* ctx);
 int amph_ctx_device(const amph_ctx* ctx);
 /* Number of devices behind the context (1 unless amph_ctx_create_multi). */
 int amph_ctx_device_count(const amph_ctx* ctx);
-/* Host-path batch size in words (default 4 Mi); 0 keeps the current value.
+/* Host-path maximum batch size in words (default 4 Mi); 0 keeps the current
+ * value.  A call is cut into about 8 batches of at least 32 MiB of traffic
+ * each, at most this many words.
  * Host-pointer calls stream their arrays through the GPU batch by batch:
  * pageable caller memory is staged through page-locked buffers by CPU
  * threads (AMPH_HOST_THREADS, default min(8, cores/2)) with HtoD, kernel and
