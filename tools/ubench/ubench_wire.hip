@@ -24,11 +24,14 @@ void run_rv(const TextSet& tx, size_t W, size_t nc, uint32_t pad, uint4* out, un
   hipLaunchKernelGGL((k_rv_b64<NP, true, BS>), dim3((unsigned)((W + Wire<BS>::words - 1) / Wire<BS>::words)),
                      dim3(BS), 0, 0, tx, NP, W, nc, pad, out, fl, fl + 1, f);
 }
+static int g_mask_out = 0;  // argv[2]: 0 = records (24 B), 1 = raw words (16 B), 2 = no output (verify only)
 template <int NP, int BS>
 void run_mask(const TextSet& tx, size_t W, size_t nc, uint32_t pad, const uint4* sec, char* rec,
               unsigned long long* fl, Fp f) {
+  uint4* o16 = g_mask_out == 1 ? (uint4*)rec : nullptr;
+  char* o24 = g_mask_out == 0 ? rec : nullptr;
   hipLaunchKernelGGL((k_mask_b64<NP, true, BS>), dim3((unsigned)((W + Wire<BS>::words - 1) / Wire<BS>::words)),
-                     dim3(BS), 0, 0, tx, NP, W, nc, pad, sec, W, (uint4*)nullptr, rec, fl, fl + 1, f);
+                     dim3(BS), 0, 0, tx, NP, W, nc, pad, sec, W, o16, o24, fl, fl + 1, f);
 }
 
 template <int NP>
@@ -101,6 +104,7 @@ void sweep(size_t W, int R, Fp f) {
 
 int main(int argc, char** argv) {
   const int R = argc > 1 ? atoi(argv[1]) : 20;
+  g_mask_out = argc > 2 ? atoi(argv[2]) : 0;
   Fp f = test_fp();
   sweep<2>((size_t)1 << 20, R, f);
   sweep<2>((size_t)1 << 24, R, f);
