@@ -112,6 +112,10 @@ def _load():
     L.amph_party_finish_b64.argtypes = [vp, i32, C.POINTER(vp)]
     L.amph_party_free.restype = None
     L.amph_party_free.argtypes = [vp]
+    L.amph_party_begin_dev.argtypes = [vp, vp, sz, vp, vp, sz, i32, vp, vp, vp, vp, C.POINTER(vp)]
+    L.amph_party_text_dev.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
+    L.amph_party_partner_dev.argtypes = [vp, i32, vp, sz, vp, vp]
+    L.amph_party_finish_b64_dev.argtypes = [vp, i32, C.POINTER(vp), vp]
     return L
 
 
@@ -130,7 +134,8 @@ EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count",
             "amph_exchange_encode", "amph_exchange_decode", "amph_stream_probe",
             "amph_recombine_verify_b64", "amph_mask_input_b64", "amph_party_begin", "amph_party_words", "amph_party_text_len",
             "amph_party_text", "amph_party_partner", "amph_party_finish", "amph_party_finish_b64",
-            "amph_party_free"]
+            "amph_party_free", "amph_party_begin_dev", "amph_party_text_dev", "amph_party_partner_dev",
+            "amph_party_finish_b64_dev"]
 
 
 class TimingEvent:
@@ -607,6 +612,26 @@ class Context:
                                          *[_ptr(x) for x in yrv], C.byref(h)))
         return PartySession(self, h, W, n_parties, yrv)
 
+    def party_begin_dev(self, share_data, share_stride: int, masks32, triples96, n_parties: int,
+                        want_yrv: bool = False) -> "PartySessionDev":
+        """amph_party_begin_dev on torch device tensors (used in place; the
+        triples must stay unchanged until finish), asynchronous on torch's
+        current stream."""
+        import torch
+        W = share_data.shape[0]
+        _need(share_data.is_cuda and masks32.is_cuda and triples96.is_cuda, "device tensors expected")
+        _need(share_data.numel() == W * share_stride, "share data: %d words of %d bytes" % (W, share_stride))
+        _need(masks32.numel() == 64 * W, "expected %d input-mask tuples" % (2 * W))
+        _need(triples96.numel() == 192 * W, "expected %d multiplication triples" % (2 * W))
+        yrv = tuple(torch.empty((W, 16), dtype=torch.uint8, device=share_data.device) for _ in range(3)) \
+            if want_yrv else (None, None, None)
+        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        h = C.c_void_p()
+        self._check(lib.amph_party_begin_dev(self._h, _ptr(share_data), share_stride, _ptr(masks32),
+                                             _ptr(triples96), W, n_parties, *[_ptr(x) for x in yrv], stream,
+                                             C.byref(h)))
+        return PartySessionDev(self, h, W, n_parties, yrv, (share_data, masks32, triples96))
+
     # -- synthetic device inputs (bench / tests) --------------------------------
     def synth_odos(self, seed: int, n: int, words: int, fault_index: int = -1,
                    noncanon_permille: int = 0, with_plain: bool = False):
@@ -687,3 +712,65 @@ class PartySession:
 
     def __exit__(self, *exc):
         self.close()
+
+
+class _DevArray:  # a device address as __cuda_array_interface__ (torch.as_tensor views it)
+    def __init__(self, ptr: int, n: int, typestr: str):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False), "version": 2}
+
+
+def _dev_view(ptr: int, n: int, typestr: str, device: int):
+    import torch
+    return torch.as_tensor(_DevArray(ptr, n, typestr), device="cuda:%d" % device)
+
+
+class PartySessionDev(PartySession):
+    """A device-mode amph_party (amph_party_*_dev): torch device tensors in
+    and out, every call asynchronous on torch's current stream."""
+
+    def __init__(self, ctx: Context, h, words: int, n_parties: int, yrv, keep):
+        super().__init__(ctx, h, words, n_parties, yrv)
+        self._keep = keep  # the tuples, read in place until finish
+
+    def _stream(self):
+        import torch
+        return C.c_void_p(torch.cuda.current_stream(self.ctx.device).cuda_stream)
+
+    def text_dev(self):
+        """-> (this party's text: a uint8 device tensor of the text's capacity,
+        its length: an int64 (1,) device tensor), both views of session memory
+        (amph_party_text_dev), valid once the stream has run begin."""
+        t, n = C.c_void_p(), C.c_void_p()
+        Context._check(lib.amph_party_text_dev(self._h, C.byref(t), C.byref(n)))
+        cap = lib.amph_exchange_max_chars(2 * self.words)
+        return _dev_view(t.value, cap, "|u1", self.ctx.device), _dev_view(n.value, 1, "<i8", self.ctx.device)
+
+    def text(self) -> bytes:
+        """Synchronises and copies this party's text to the host (tests)."""
+        t, n = self.text_dev()
+        L = int(n.item())
+        return t[:L].cpu().numpy().tobytes()
+
+    def partner(self, slot: int, text, bad=None):
+        """A partner's text (a uint8 device tensor) into slot 1..n-1; bad: an
+        int64 (1,) device tensor the decode reports into (returned)."""
+        import torch
+        if bad is None:
+            bad = torch.empty(1, dtype=torch.int64, device=text.device)
+        Context._check(lib.amph_party_partner_dev(self._h, slot, _ptr(text) if text.numel() else None,
+                                                  text.numel(), _ptr(bad), self._stream()))
+        return bad
+
+    def finish(self, is_player0: bool):
+        raise AmphoraNativeError(AMPH_E_PARAM, "a device-mode session finishes with finish_b64")
+
+    def finish_b64(self, is_player0: bool, out=None):
+        """-> the five fields' base64 text as uint8 device tensors (or into out)."""
+        import torch
+        nc = 4 * ((16 * self.words + 2) // 3)
+        dev = self._keep[0].device
+        outs = out if out is not None else [torch.empty(max(nc, 1), dtype=torch.uint8, device=dev) for _ in range(5)]
+        arr = (C.c_void_p * 5)(*[_ptr(o) for o in outs])
+        Context._check(lib.amph_party_finish_b64_dev(self._h, int(is_player0), arr, self._stream()))
+        return [o[:nc] for o in outs]
+

@@ -1826,21 +1826,29 @@ int amph_synth_words(amph_ctx* c, uint64_t seed, size_t count, uint8_t* out, voi
 
 // ---- one party's Output Delivery, device-resident between steps ----------------
 // (include/amphora.h, "one party's Output Delivery with device-resident state")
-// Device memory: one allocation carved into the triples, the five ODO fields,
-// every party's diffs, this party's text and the encoder's scratch; the share
-// data and masks live in a second one released once begin has run; partner
-// texts, the decoder's scratch and the base64 output share a third, grown as
-// needed.  Every copy is a blocking hipMemcpy issued with the context's stream
-// idle (kPageableRule), so caller buffers may be pageable or page-locked.
+// Device memory: one allocation carved into the triples (host mode), the five
+// ODO fields, this party's diffs, its text and the encoder's scratch; the share
+// data and masks live in a second one released once begin has run; each
+// partner's diffs (the exchange decode's span form, amph::XSpans) and its
+// decode scratch in one allocation per slot, sized by its text; partner texts
+// and the base64 output staged in a fourth (host mode).  Host mode: every copy
+// is a blocking hipMemcpy issued with the context's stream idle
+// (kPageableRule), so caller buffers may be pageable or page-locked.  Device
+// mode (amph_party_*_dev): nothing is copied; the caller's buffers are used in
+// place and every launch goes on the caller's stream.
 struct amph_party {
   amph_ctx* c = nullptr;
   size_t W = 0;
   int n = 0;
+  bool dev = false;               // device mode
+  hipStream_t dstream = nullptr;  // device mode: the stream of the latest call
   DevBuf mem, tmp, io;
   const uint4* triples = nullptr;
   uint4* f5[5] = {};  // y, r, v, w, u
   uint4* mag[AMPH_MAX_PARTIES] = {};
   uint8_t* neg[AMPH_MAX_PARTIES] = {};
+  DevBuf pbuf[AMPH_MAX_PARTIES];
+  amph::XSpans xs[AMPH_MAX_PARTIES] = {};
   char* text = nullptr;
   unsigned long long* text_len_dev = nullptr;
   void* enc_scratch = nullptr;
@@ -1851,6 +1859,7 @@ struct amph_party {
     mem.release();
     tmp.release();
     io.release();
+    for (DevBuf& b : pbuf) b.release();
   }
 };
 
@@ -1863,49 +1872,25 @@ int party_check(amph_party* p) {
   return AMPH_OK;
 }
 
-// the summed diffs -> w, u on the device (every partner's text must be in)
-int party_open_post(amph_party* p, int is_player0, hipStream_t s) {
-  const uint32_t all = p->n >= 32 ? ~0u : ((1u << p->n) - 1u);
-  if ((p->have & all) != all) {
-    int j = 1;
-    while (j < p->n && (p->have >> j & 1u)) ++j;
-    return fail(AMPH_E_PARAM, "partner slot " + std::to_string(j) + "'s interimValues text is missing");
-  }
-  amph::SignedSet set{};
-  for (int j = 0; j < p->n; ++j) {
-    set.mag[j] = p->mag[j];
-    set.neg[j] = (const uint32_t*)p->neg[j];
-  }
-  hipError_t e = amph::launch_open_post(set, p->n, p->triples, p->W, is_player0, p->f5[3], p->f5[4], p->c->f,
-                                        cfg(p->c, s, p->W));
-  return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_open_post");
-}
-}  // namespace
-
-extern "C" {
-
-int amph_party_begin(amph_ctx* c, const uint8_t* share_data, size_t share_stride, const uint8_t* masks,
-                     const uint8_t* triples, size_t words, int n_parties, uint8_t* oy, uint8_t* orr,
-                     uint8_t* ov, amph_party** out) {
+int party_args(amph_ctx* c, size_t share_stride, int n_parties, size_t words, const void* share_data,
+               const void* masks, const void* triples, amph_party** out) {
   if (!out) return fail(AMPH_E_PARAM, "null session output");
   *out = nullptr;
   if (check_ctx(c)) return AMPH_E_PARAM;
   if (share_stride != 16 && share_stride != 32) return fail(AMPH_E_PARAM, "share_stride must be 16 or 32");
   if (n_parties < 1 || n_parties > AMPH_MAX_PARTIES) return fail(AMPH_E_PARAM, "n_parties must be in [1, 16]");
   if (words && (!share_data || !masks || !triples)) return fail(AMPH_E_PARAM, "null buffer");
-  if (!c->sub.empty()) c = c->sub[0];  // a multi-device context runs sessions on its first device
-  HIP_TRY(use_device(c->device));
-  std::lock_guard<std::mutex> g(c->mu);
-  std::unique_ptr<amph_party> p(new amph_party);
-  p->c = c;
-  p->W = words;
-  p->n = n_parties;
-  const size_t W = words, P = 2 * words;
-  const size_t sz[] = {192 * W, 16 * W, 16 * W, 16 * W, 16 * W, 16 * W,
-                       amph::xenc_max_bytes(P), 8, amph::xenc_scratch_bytes(P)};
+  return AMPH_OK;
+}
+
+// the session's device memory; yrv[k] non-null: field k lives in the caller's
+// device buffer (device mode), else in the session's
+int party_alloc(amph_party* p, bool copy_triples, uint8_t* const yrv[3]) {
+  const size_t W = p->W, P = 2 * W;
+  const size_t sz[] = {copy_triples ? 192 * W : 0, 16 * W, 16 * W, 16 * W, 16 * W, 16 * W,
+                       amph::xenc_max_bytes(P), 8, amph::xenc_scratch_bytes(P), 64 * W, 4 * W};
   size_t total = 0;
   for (size_t b : sz) total += align256(b ? b : 16);
-  for (int j = 0; j < n_parties; ++j) total += align256(64 * W ? 64 * W : 16) + align256(4 * W ? 4 * W : 16);
   if (p->mem.ensure(total) != hipSuccess) return fail(AMPH_E_NOMEM, "party session device memory");
   uint8_t* cur = (uint8_t*)p->mem.p;
   auto take = [&](size_t b) {
@@ -1914,14 +1899,133 @@ int amph_party_begin(amph_ctx* c, const uint8_t* share_data, size_t share_stride
     return q;
   };
   p->triples = (const uint4*)take(sz[0]);
-  for (int k = 0; k < 5; ++k) p->f5[k] = (uint4*)take(sz[1 + k]);
+  for (int k = 0; k < 5; ++k) {
+    uint4* own = (uint4*)take(sz[1 + k]);
+    p->f5[k] = k < 3 && yrv[k] ? (uint4*)yrv[k] : own;
+  }
   p->text = (char*)take(sz[6]);
   p->text_len_dev = (unsigned long long*)take(sz[7]);
   p->enc_scratch = take(sz[8]);
-  for (int j = 0; j < n_parties; ++j) {
-    p->mag[j] = (uint4*)take(64 * W);
-    p->neg[j] = take(4 * W);
+  p->mag[0] = (uint4*)take(sz[9]);
+  p->neg[0] = take(sz[10]);
+  return AMPH_OK;
+}
+
+// k_odo_pre (y, r, v + this party's diffs) and the exchange encode of the diffs
+int party_pre(amph_party* p, const uint8_t* dshare, size_t share_stride, const uint8_t* dmasks, hipStream_t s) {
+  amph_ctx* c = p->c;
+  const size_t W = p->W, P = 2 * W;
+  hipError_t e = amph::launch_odo_pre((const uint4*)dshare, (int)(share_stride / 16), (const uint4*)dmasks,
+                                      p->triples, W, p->f5[0], p->f5[1], p->f5[2], p->mag[0],
+                                      (uint32_t*)p->neg[0], c->f, cfg(c, s, W));
+  if (e != hipSuccess) return hip_fail(e, "k_odo_pre");
+  e = amph::launch_exchange_encode(p->mag[0], p->neg[0], P, p->text, p->text_len_dev, p->enc_scratch,
+                                   cfg(c, s, P));
+  return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_xenc");
+}
+
+int party_slot_check(amph_party* p, int slot, const char* text, size_t len) {
+  if (int st = party_check(p)) return st;
+  if (slot < 1 || slot >= p->n)
+    return fail(AMPH_E_PARAM, "partner slot must be in [1, " + std::to_string(p->n - 1) + "]");
+  if (p->have >> slot & 1u) return fail(AMPH_E_PARAM, "partner slot " + std::to_string(slot) + " already holds a text");
+  if (len && !text) return fail(AMPH_E_PARAM, "null text");
+  return AMPH_OK;
+}
+
+// a partner's text (device memory) decoded into the slot's span form; bad:
+// the device word the decode reports into (reset here)
+int party_decode(amph_party* p, int slot, const char* dtext, size_t len, unsigned long long* bad, hipStream_t s) {
+  const size_t P = 2 * p->W;
+  const size_t nb = amph::xspan_spans(len), slots = amph::xspan_slots(len, P);
+  const size_t xsz[5] = {16 * slots, slots, 8 * (nb + 1), 16 * amph::xspan_map_words(P),
+                         amph::xdec_spans_scratch_bytes(len)};
+  size_t xtotal = 0;
+  for (size_t b : xsz) xtotal += align256(b);
+  if (p->pbuf[slot].ensure(xtotal) != hipSuccess) return fail(AMPH_E_NOMEM, "party session partner diffs");
+  uint8_t* xp = (uint8_t*)p->pbuf[slot].p;
+  amph::XSpans& xs = p->xs[slot];
+  xs.mag = (uint4*)xp;
+  xs.neg = xp + align256(xsz[0]);
+  xs.base = (uint64_t*)(xs.neg + align256(xsz[1]));
+  xs.map = (uint4*)((uint8_t*)xs.base + align256(xsz[2]));
+  void* scratch = (uint8_t*)xs.map + align256(xsz[3]);
+  xs.nb = nb;
+  p->mag[slot] = xs.mag;
+  p->neg[slot] = xs.neg;
+  HIP_TRY(hipMemsetAsync(bad, 0x7F, 8, s));
+  hipError_t e = amph::launch_exchange_decode_spans(dtext, len, P, xs, bad, scratch, cfg(p->c, s, len));
+  return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_xdec");
+}
+
+int decode_status(int64_t bad, size_t len, size_t P, int64_t* bad_index) {
+  if (bad == (int64_t)AMPH_NO_FAILURE) return AMPH_OK;
+  if (bad_index) *bad_index = bad;
+  if ((size_t)bad == len)
+    return fail(AMPH_E_LEN, "interimValues must hold exactly " + std::to_string(P) + " FactorPairs");
+  return fail(AMPH_E_PARAM, "Malformed FactorPair JSON at offset " + std::to_string(bad));
+}
+
+int party_all_in(amph_party* p) {
+  const uint32_t all = p->n >= 32 ? ~0u : ((1u << p->n) - 1u);
+  if ((p->have & all) == all) return AMPH_OK;
+  int j = 1;
+  while (j < p->n && (p->have >> j & 1u)) ++j;
+  return fail(AMPH_E_PARAM, "partner slot " + std::to_string(j) + "'s interimValues text is missing");
+}
+
+// the summed diffs -> w, u on the device (every partner's text must be in)
+int party_open_post(amph_party* p, int is_player0, hipStream_t s) {
+  if (int st = party_all_in(p)) return st;
+  amph::SignedSet set{};
+  for (int j = 0; j < p->n; ++j) {
+    set.mag[j] = p->mag[j];
+    set.neg[j] = (const uint32_t*)p->neg[j];
+    if (j > 0) {
+      set.sbase[j] = p->xs[j].base;
+      set.smap[j] = p->xs[j].map;
+      set.snb[j] = p->xs[j].nb;
+    }
   }
+  hipError_t e = amph::launch_open_post(set, p->n, p->triples, p->W, is_player0, p->f5[3], p->f5[4], p->c->f,
+                                        cfg(p->c, s, p->W));
+  return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_open_post");
+}
+
+// the five fields as base64 text into out[k] (device memory)
+int party_b64(amph_party* p, char* const out[5], hipStream_t s) {
+  const size_t nb = 16 * p->W;
+  for (int k = 0; k < 5 && nb; ++k) {
+    hipError_t e = amph::launch_b64_encode((const uint8_t*)p->f5[k], nb, out[k], cfg(p->c, s, (nb + 11) / 12));
+    if (e != hipSuccess) return hip_fail(e, "k_b64_encode");
+  }
+  return AMPH_OK;
+}
+
+int party_mode(amph_party* p, bool dev) {
+  if (p->dev != dev)
+    return fail(AMPH_E_PARAM, dev ? "a host-mode party session takes the host calls"
+                                  : "a device-mode party session takes the *_dev calls");
+  return AMPH_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int amph_party_begin(amph_ctx* c, const uint8_t* share_data, size_t share_stride, const uint8_t* masks,
+                     const uint8_t* triples, size_t words, int n_parties, uint8_t* oy, uint8_t* orr,
+                     uint8_t* ov, amph_party** out) {
+  if (int st = party_args(c, share_stride, n_parties, words, share_data, masks, triples, out)) return st;
+  if (!c->sub.empty()) c = c->sub[0];  // a multi-device context runs sessions on its first device
+  HIP_TRY(use_device(c->device));
+  std::lock_guard<std::mutex> g(c->mu);
+  std::unique_ptr<amph_party> p(new amph_party);
+  p->c = c;
+  p->W = words;
+  p->n = n_parties;
+  const size_t W = words;
+  uint8_t* const none[3] = {nullptr, nullptr, nullptr};
+  if (int st = party_alloc(p.get(), true, none)) return st;
   if (p->tmp.ensure(align256(share_stride * W + 16) + align256(64 * W + 16)) != hipSuccess)
     return fail(AMPH_E_NOMEM, "party session staging");
   uint8_t* dshare = (uint8_t*)p->tmp.p;
@@ -1934,13 +2038,7 @@ int amph_party_begin(amph_ctx* c, const uint8_t* share_data, size_t share_stride
     HIP_TRY(hipMemcpy(dmasks, masks, 64 * W, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy((void*)p->triples, triples, 192 * W, hipMemcpyHostToDevice));
   }
-  hipError_t e = amph::launch_odo_pre((const uint4*)dshare, (int)(share_stride / 16), (const uint4*)dmasks,
-                                      p->triples, W, p->f5[0], p->f5[1], p->f5[2], p->mag[0],
-                                      (uint32_t*)p->neg[0], c->f, cfg(c, s, W));
-  if (e != hipSuccess) return hip_fail(e, "k_odo_pre");
-  e = amph::launch_exchange_encode(p->mag[0], p->neg[0], P, p->text, p->text_len_dev, p->enc_scratch,
-                                   cfg(c, s, P));
-  if (e != hipSuccess) return hip_fail(e, "k_xenc");
+  if (int st = party_pre(p.get(), dshare, share_stride, dmasks, s)) return st;
   uint64_t len = 0;
   HIP_TRY(read_back(s, {{&len, p->text_len_dev, 8}, {oy, p->f5[0], oy ? 16 * W : 0},
                         {orr, p->f5[1], orr ? 16 * W : 0}, {ov, p->f5[2], ov ? 16 * W : 0}}));
@@ -1953,10 +2051,11 @@ int amph_party_begin(amph_ctx* c, const uint8_t* share_data, size_t share_stride
 
 size_t amph_party_words(const amph_party* p) { return p ? p->W : 0; }
 
-uint64_t amph_party_text_len(const amph_party* p) { return p ? p->text_len : 0; }
+uint64_t amph_party_text_len(const amph_party* p) { return p && !p->dev ? p->text_len : 0; }
 
 int amph_party_text(amph_party* p, char* out, size_t out_cap) {
   if (!p || !p->c) return fail(AMPH_E_PARAM, "null party session");
+  if (int st = party_mode(p, false)) return st;
   if (!out && p->text_len) return fail(AMPH_E_PARAM, "null output");
   if (out_cap < p->text_len)
     return fail(AMPH_E_LEN, "output capacity " + std::to_string(out_cap) + " below the text length " +
@@ -1972,42 +2071,29 @@ int amph_party_text(amph_party* p, char* out, size_t out_cap) {
 
 int amph_party_partner(amph_party* p, int slot, const char* text, size_t len, int64_t* bad_index) {
   if (bad_index) *bad_index = -1;
-  if (int st = party_check(p)) return st;
-  if (slot < 1 || slot >= p->n)
-    return fail(AMPH_E_PARAM, "partner slot must be in [1, " + std::to_string(p->n - 1) + "]");
-  if (p->have >> slot & 1u) return fail(AMPH_E_PARAM, "partner slot " + std::to_string(slot) + " already holds a text");
-  if (len && !text) return fail(AMPH_E_PARAM, "null text");
+  if (int st = party_slot_check(p, slot, text, len)) return st;
+  if (int st = party_mode(p, false)) return st;
   amph_ctx* c = p->c;
   HIP_TRY(use_device(c->device));
   std::lock_guard<std::mutex> g(c->mu);
-  const size_t P = 2 * p->W, sbytes = amph::xdec_scratch_bytes(len);
-  if (p->io.ensure(align256(len + 16) + 256 + align256(sbytes)) != hipSuccess)
-    return fail(AMPH_E_NOMEM, "party session text staging");
+  if (p->io.ensure(align256(len + 16) + 256) != hipSuccess) return fail(AMPH_E_NOMEM, "party session text staging");
   uint8_t* dtext = (uint8_t*)p->io.p;
   unsigned long long* dbad = (unsigned long long*)(dtext + align256(len + 16));
-  void* scratch = dtext + align256(len + 16) + 256;
   hipStream_t s;
   if (int st = host_stream0(c, &s)) return st;
   HIP_TRY(hipStreamSynchronize(s));
   if (len) HIP_TRY(hipMemcpy(dtext, text, len, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemsetAsync(dbad, 0x7F, 8, s));
-  hipError_t e = amph::launch_exchange_decode((const char*)dtext, len, P, p->mag[slot], p->neg[slot], dbad, scratch,
-                                              cfg(c, s, len));
-  if (e != hipSuccess) return hip_fail(e, "k_xdec");
+  if (int st = party_decode(p, slot, (const char*)dtext, len, dbad, s)) return st;
   int64_t bad = 0;
   HIP_TRY(read_back(s, {{&bad, dbad, 8}}));
-  if (bad != (int64_t)AMPH_NO_FAILURE) {
-    if (bad_index) *bad_index = bad;
-    if ((size_t)bad == len)
-      return fail(AMPH_E_LEN, "interimValues must hold exactly " + std::to_string(P) + " FactorPairs");
-    return fail(AMPH_E_PARAM, "Malformed FactorPair JSON at offset " + std::to_string(bad));
-  }
+  if (int st = decode_status(bad, len, 2 * p->W, bad_index)) return st;
   p->have |= 1u << slot;
   return AMPH_OK;
 }
 
 int amph_party_finish(amph_party* p, int is_player0, uint8_t* ow, uint8_t* ou) {
   if (int st = party_check(p)) return st;
+  if (int st = party_mode(p, false)) return st;
   if (p->W && (!ow || !ou)) return fail(AMPH_E_PARAM, "null output");
   amph_ctx* c = p->c;
   HIP_TRY(use_device(c->device));
@@ -2022,6 +2108,7 @@ int amph_party_finish(amph_party* p, int is_player0, uint8_t* ow, uint8_t* ou) {
 
 int amph_party_finish_b64(amph_party* p, int is_player0, char* const fields_b64[5]) {
   if (int st = party_check(p)) return st;
+  if (int st = party_mode(p, false)) return st;
   if (!fields_b64) return fail(AMPH_E_PARAM, "null field array");
   for (int k = 0; k < 5; ++k)
     if (p->W && !fields_b64[k]) return fail(AMPH_E_PARAM, "null field text");
@@ -2034,12 +2121,73 @@ int amph_party_finish_b64(amph_party* p, int is_player0, char* const fields_b64[
   if (int st = host_stream0(c, &s)) return st;
   if (int st = party_open_post(p, is_player0, s)) return st;
   char* d = (char*)p->io.p;
-  for (int k = 0; k < 5 && nb; ++k) {
-    hipError_t e = amph::launch_b64_encode((const uint8_t*)p->f5[k], nb, d + k * stride, cfg(c, s, (nb + 11) / 12));
-    if (e != hipSuccess) return hip_fail(e, "k_b64_encode");
-  }
+  char* const dout[5] = {d, d + stride, d + 2 * stride, d + 3 * stride, d + 4 * stride};
+  if (int st = party_b64(p, dout, s)) return st;
   HIP_TRY(read_back(s, {{fields_b64[0], d, nc}, {fields_b64[1], d + stride, nc}, {fields_b64[2], d + 2 * stride, nc},
                         {fields_b64[3], d + 3 * stride, nc}, {fields_b64[4], d + 4 * stride, nc}}));
+  p->finished = true;
+  return AMPH_OK;
+}
+
+// ---- device mode ------------------------------------------------------------------
+int amph_party_begin_dev(amph_ctx* c, const uint8_t* share_data, size_t share_stride, const uint8_t* masks,
+                         const uint8_t* triples, size_t words, int n_parties, uint8_t* oy, uint8_t* orr,
+                         uint8_t* ov, void* stream, amph_party** out) {
+  if (int st = party_args(c, share_stride, n_parties, words, share_data, masks, triples, out)) return st;
+  if (!c->sub.empty()) return fail(AMPH_E_PARAM, "device-mode sessions need a single-device context");
+  if (int st = check_dev_words({share_data, masks, triples, oy, orr, ov})) return st;
+  HIP_TRY(use_device(c->device));
+  std::lock_guard<std::mutex> g(c->mu);
+  std::unique_ptr<amph_party> p(new amph_party);
+  p->c = c;
+  p->W = words;
+  p->n = n_parties;
+  p->dev = true;
+  p->dstream = (hipStream_t)stream;
+  uint8_t* const yrv[3] = {oy, orr, ov};
+  if (int st = party_alloc(p.get(), false, yrv)) return st;
+  p->triples = (const uint4*)triples;
+  if (int st = party_pre(p.get(), share_data, share_stride, masks, p->dstream)) return st;
+  p->have = 1u;
+  *out = p.release();
+  return AMPH_OK;
+}
+
+int amph_party_text_dev(amph_party* p, const char** text, const uint64_t** len) {
+  if (!p || !p->c) return fail(AMPH_E_PARAM, "null party session");
+  if (int st = party_mode(p, true)) return st;
+  if (!text || !len) return fail(AMPH_E_PARAM, "null output");
+  *text = p->text;
+  *len = (const uint64_t*)p->text_len_dev;
+  return AMPH_OK;
+}
+
+int amph_party_partner_dev(amph_party* p, int slot, const char* text, size_t len, int64_t* bad_index,
+                           void* stream) {
+  if (int st = party_slot_check(p, slot, text, len)) return st;
+  if (int st = party_mode(p, true)) return st;
+  if (!bad_index || ((uintptr_t)bad_index & 7)) return fail(AMPH_E_PARAM, "bad_index must be an 8-byte aligned device word");
+  amph_ctx* c = p->c;
+  HIP_TRY(use_device(c->device));
+  std::lock_guard<std::mutex> g(c->mu);
+  p->dstream = (hipStream_t)stream;
+  if (int st = party_decode(p, slot, text, len, (unsigned long long*)bad_index, p->dstream)) return st;
+  p->have |= 1u << slot;
+  return AMPH_OK;
+}
+
+int amph_party_finish_b64_dev(amph_party* p, int is_player0, char* const fields_b64[5], void* stream) {
+  if (int st = party_check(p)) return st;
+  if (int st = party_mode(p, true)) return st;
+  if (!fields_b64) return fail(AMPH_E_PARAM, "null field array");
+  for (int k = 0; k < 5; ++k)
+    if (p->W && !fields_b64[k]) return fail(AMPH_E_PARAM, "null field text");
+  amph_ctx* c = p->c;
+  HIP_TRY(use_device(c->device));
+  std::lock_guard<std::mutex> g(c->mu);
+  p->dstream = (hipStream_t)stream;
+  if (int st = party_open_post(p, is_player0, p->dstream)) return st;
+  if (int st = party_b64(p, fields_b64, p->dstream)) return st;
   p->finished = true;
   return AMPH_OK;
 }
@@ -2049,7 +2197,8 @@ void amph_party_free(amph_party* p) {
   if (p->c) {
     (void)use_device(p->c->device);
     std::lock_guard<std::mutex> g(p->c->mu);
-    if (p->c->streams[0]) (void)hipStreamSynchronize(p->c->streams[0]);
+    if (p->dev) (void)hipStreamSynchronize(p->dstream);
+    else if (p->c->streams[0]) (void)hipStreamSynchronize(p->c->streams[0]);
   }
   delete p;
 }

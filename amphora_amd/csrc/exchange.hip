@@ -211,6 +211,9 @@ __device__ __forceinline__ char* put_digits(char* o, const uint32_t (&ch)[5], in
 }
 
 // ---- device-wide exclusive scan of u64 (three passes) ----------------------------
+// Decode count words: colon count in bits 0..39, spans with whitespace (count
+// pass) or outside the compact layout (k_xdec_span) from bit 40
+constexpr uint64_t kWsBit = 1ull << 40, kCountMask = kWsBit - 1;
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
   const int lane = __lane_id();
 #pragma unroll
@@ -276,6 +279,17 @@ __device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t* tota
   return r;
 }
 
+// The decode's span form: with x the spans' colon counts, map[b] = the span
+// holding value kXMapValues * b (b < nmap), written by the lane that scans
+// that span.
+__device__ __forceinline__ void span_map(uint4* map, size_t nmap, size_t span, uint64_t e, uint64_t c) {
+  if (!map) return;
+  e &= kCountMask;
+  c &= kCountMask;
+  for (size_t b = (e + kXMapValues - 1) / kXMapValues; b < nmap && b * kXMapValues < e + c; ++b)
+    map[b].x = (uint32_t)span;  // (k_xdec_slow<SpanBases> completes the window)
+}
+
 __global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const uint64_t* x, size_t n,
                                                         uint64_t* bsum) {
   const size_t i = (size_t)blockIdx.x * kScanBlock + threadIdx.x;
@@ -284,27 +298,37 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const uint64_t* x, s
   if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-// One workgroup: in-place exclusive scan of n values, x[n] = total.
-__global__ __launch_bounds__(kScanBlock) void k_scan_single(uint64_t* x, size_t n) {
+// One workgroup: in-place exclusive scan of n values, x[n] = total (map as
+// k_scan_apply's).
+__global__ __launch_bounds__(kScanBlock) void k_scan_single(uint64_t* x, size_t n, uint4* map,
+                                                        size_t nmap) {
   uint64_t carry = 0;
   for (size_t base = 0; base < n; base += kScanBlock) {
     const size_t i = base + threadIdx.x;
     const uint64_t v = i < n ? x[i] : 0;
     uint64_t total;
     const uint64_t e = block_excl_scan(v, &total);
-    if (i < n) x[i] = carry + e;
+    if (i < n) {
+      x[i] = carry + e;
+      span_map(map, nmap, i, carry + e, v);
+    }
     carry += total;
   }
   if (threadIdx.x == 0) x[n] = carry;
 }
 
-// x[i] <- exclusive prefix (bsum already scanned); x[n] <- total
+// x[i] <- exclusive prefix (bsum already scanned); x[n] <- total (+ the map)
 __global__ __launch_bounds__(kScanBlock) void k_scan_apply(uint64_t* x, size_t n,
-                                                       const uint64_t* bsum, size_t nb) {
+                                                       const uint64_t* bsum, size_t nb,
+                                                       uint4* map, size_t nmap) {
   const size_t i = (size_t)blockIdx.x * kScanBlock + threadIdx.x;
   uint64_t total;
-  const uint64_t e = block_excl_scan(i < n ? x[i] : 0, &total);
-  if (i < n) x[i] = bsum[blockIdx.x] + e;
+  const uint64_t v = i < n ? x[i] : 0;
+  const uint64_t e = block_excl_scan(v, &total);
+  if (i < n) {
+    x[i] = bsum[blockIdx.x] + e;
+    span_map(map, nmap, i, bsum[blockIdx.x] + e, v);
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) x[n] = bsum[nb];
 }
 
@@ -469,8 +493,6 @@ constexpr int kWin = (int)kDecSpan + 2 * kWinPad;      // staged bytes
 // 256-lane workgroup.  96 us per 640 MB text where 128 lanes x 64
 // lane-contiguous bytes per span took 162 (tools/ubench/ubench_xcount.hip).
 constexpr int kCntWaves = 4;
-// bsum / bscan words: colon count in bits 0..39, spans with whitespace from bit 40
-constexpr uint64_t kWsBit = 1ull << 40, kCountMask = kWsBit - 1;
 
 __device__ __forceinline__ uint32_t swar_below21(uint32_t w) {  // nonzero iff some byte < 0x21
   return (w - 0x21212121u) & ~w & 0x80808080u;
@@ -758,6 +780,68 @@ __device__ __forceinline__ bool fast_segment(const uint32_t* l32, uint32_t o, ui
   });
 }
 
+// fast_segment without the value's global index (k_xdec_span parses with no
+// count pass before it): the member comes from the byte before the key's
+// quote ('{' member 0, ',' member 1 -- that byte ends the previous value's
+// segment, which checks it).  Returns SEG_OK when the member's own form holds:
+// member 0 followed by ',' "K" ':' (K the other key), member 1 by '}' ',' '{'
+// "K" ':' (SEG_MID) or by '}' ']' and the end of the text (SEG_LAST); SEG_FIRST
+// when the value opens the text ("[{" before its key, 6th byte).  Since every
+// value's segment reaches the next value's colon, a text whose values all hold
+// alternates member 0 / member 1 from its first value (which must be SEG_FIRST)
+// to its last (which can only be SEG_LAST), so no check needs the index; the
+// array check adds the count.
+enum : uint32_t { SEG_OK = 1, SEG_M1 = 2, SEG_FIRST = 4, SEG_LAST = 8, SEG_MID = 16 };
+
+__device__ __forceinline__ uint32_t fast_value(const uint32_t* l32, uint32_t o, size_t xo, size_t len,
+                                               FastNum& r) {
+  const uint32_t pre = lds_dword(l32, o - 5);  // bytes o-5 .. o-2: '{'|',' '"' k '"'
+  r.key = (pre >> 16) & 0xFFu;
+  const uint32_t lead = pre & 0xFFu;
+  const bool m1 = lead == (uint32_t)',';
+  bool ok = (pre & 0xFF00FF00u) == 0x22002200u && (r.key == 'a' || r.key == 'b') &&
+            (lead == (uint32_t)'{' || m1) && (lds_dword(l32, o - 1) & 0xFFu) == (uint32_t)':';
+  uint32_t flags = m1 ? SEG_M1 : 0;
+  if (xo == 6 && (lds_dword(l32, o - 6) & 0xFFFFu) == 0x7B5Bu) flags |= SEG_FIRST;  // "[{"
+  const uint32_t key = r.key;
+  ok = fast_parse(l32, o, ok, r, [&](uint32_t dend) {
+    const uint32_t a0 = lds_dword(l32, dend), a1 = lds_dword(l32, dend + 4);
+    if (!m1) {  // NUM ',' '"' K '"' ':', K the other key
+      const uint32_t k = (a0 >> 16) & 0xFFu;
+      return (a0 & 0xFF00FFFFu) == 0x2200222Cu && (k == 'a' || k == 'b') && k != key &&
+             (a1 & 0xFFu) == (uint32_t)':';
+    }
+    if ((a0 & 0xFFFFu) == 0x5D7Du && xo + (dend - o) + 2 == len) flags |= SEG_LAST;  // "}]" + end
+    const uint32_t k = a1 & 0xFFu;
+    if (a0 == 0x227B2C7Du && (a1 & 0x00FFFF00u) == 0x003A2200u && (k == 'a' || k == 'b')) flags |= SEG_MID;
+    return (flags & (SEG_LAST | SEG_MID)) != 0;
+  });
+  return ok ? flags | SEG_OK : flags;
+}
+
+// The array holds exactly nvals numbers and is bracketed; an empty array
+// holds nothing but whitespace (with numbers, the lanes of the decode passes
+// check the rest).  Run by workgroup 0 of k_xdec_slow (256 lanes) before it
+// decides whether to return: one launch fewer per decode.
+__device__ __forceinline__ void array_check(const Text& t, uint64_t total, size_t nvals, unsigned long long* bad) {
+  __shared__ size_t az[2];
+  if (threadIdx.x == 0) {
+    size_t a = t.mis;
+    while (a < t.L && is_ws(t[a])) ++a;
+    size_t z = t.L;
+    while (z > t.mis && is_ws(t[z - 1])) --z;
+    if (a >= t.L || t[a] != '[') atomicMin(bad, (unsigned long long)(a - t.mis));
+    else if (z <= a + 1 || t[z - 1] != ']') atomicMin(bad, (unsigned long long)(z > t.mis ? z - 1 - t.mis : 0));
+    else if (total != nvals) atomicMin(bad, (unsigned long long)(t.L - t.mis));
+    az[0] = a + 1;
+    az[1] = z > t.mis ? z - 1 : t.mis;
+  }
+  __syncthreads();
+  if (nvals == 0)
+    for (size_t i = az[0] + threadIdx.x; i < az[1]; i += blockDim.x)
+      if (!is_ws(t[i])) atomicMin(bad, (unsigned long long)(i - t.mis));
+}
+
 // Pass 3, general (k_xdec_slow, one workgroup per span; its workgroups
 // return at once unless k_xdec_fast found a value outside the compact
 // layout): each
@@ -797,6 +881,37 @@ struct ScanBases {
     return *slow == 0 && (bscan[nb] & ~kCountMask) == 0;
   }
   __device__ __forceinline__ uint64_t base(size_t span) const { return bscan[span] & kCountMask; }
+  __device__ __forceinline__ uint64_t total() const { return bscan[nb] & kCountMask; }
+  __device__ __forceinline__ void windows() const {}
+};
+// After k_xdec_span: the general pass runs when a span's count word carries
+// the fail bit, or when the text holds other than nvals values (it then
+// reports the first value beyond nvals, as after the count pass).  When the
+// span form holds, its workgroups first complete the map's windows (XSpans)
+// from the scanned bases.
+struct SpanBases {
+  const uint64_t* bscan;
+  size_t nb, nvals;
+  uint4* map;
+  __device__ __forceinline__ void windows() const {
+    if (bscan[nb] != nvals) return;  // fail bits or a count mismatch: pair order
+    auto at = [&](size_t s, uint64_t v0, uint64_t cap) -> uint32_t {
+      return (uint32_t)(s <= nb ? min(bscan[s] - v0, cap) : cap);
+    };
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x; b * kXMapValues < nvals; b += stride) {
+      const uint32_t s0 = map[b].x;
+      const uint64_t v0 = b * kXMapValues;
+      map[b] = make_uint4(s0, (uint32_t)(v0 - bscan[s0]), at(s0 + 1, v0, 0xFFFF) | (at(s0 + 2, v0, 0xFFFF) << 16),
+                          at(s0 + 3, v0, 0xFFFFFFFFu));
+    }
+  }
+  __device__ __forceinline__ bool skip(const unsigned int*) const {
+    const uint64_t t = bscan[nb];
+    return (t & ~kCountMask) == 0 && (t & kCountMask) == nvals;
+  }
+  __device__ __forceinline__ uint64_t base(size_t span) const { return bscan[span] & kCountMask; }
+  __device__ __forceinline__ uint64_t total() const { return bscan[nb] & kCountMask; }
 };
 
 template <class Bases>
@@ -804,6 +919,8 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_slow(Text text, Bases bs, si
                                                      size_t nvals, uint4* mag, uint8_t* neg,
                                                      unsigned long long* bad,
                                                      const unsigned int* slow) {
+  if (blockIdx.x == 0) array_check(text, bs.total(), nvals, bad);
+  bs.windows();
   if (bs.skip(slow)) return;  // the compact pass held
   __shared__ uint4 win4[kWin / 16 + 1];
   __shared__ uint16_t pos[kMaxStarts];   // start, relative to b0
@@ -1026,48 +1143,78 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64
   if (__ballot(fail) != 0 && __lane_id() == 0) atomicOr(slow, 1u);
 }
 
-// The array holds exactly nvals numbers and is bracketed; an empty array
-// holds nothing but whitespace (with numbers, the lanes above check the rest).
-struct ScanTotal {
-  const uint64_t* bscan;
-  size_t nb;
-  __device__ __forceinline__ uint64_t total() const { return bscan[nb] & kCountMask; }
-};
-
-template <class Totals>
-__global__ __launch_bounds__(256) void k_xdec_check(Text t, Totals tot, size_t nvals,
-                                                    unsigned long long* bad) {
-  __shared__ size_t az[2];
-  __shared__ uint64_t stotal;
-  if (threadIdx.x < 64) {
-    const uint64_t v = tot.total();
-    if (threadIdx.x == 0) stotal = v;
+// The decode into span form (launch_exchange_decode_spans; the party
+// session's partner texts), ONE read of the text with no count pass before
+// it: staging and colon listing as k_xdec_fast, then each value checked
+// against its compact-layout segment without its global index (fast_value)
+// and stored at slot kXSpanSlots * span + its rank among the span's colons,
+// its byte = sign (bit 0) | key "b" (bit 1).  cnt[span] = the span's colon
+// count, plus kWsBit when a value falls outside the compact layout, the span
+// holds more than kXSpanSlots values, or the text's first value is not the
+// span-0 value that opens it; the scan of these words gives every span its
+// first value index (and the map k_open_post starts from), and any kWsBit sends
+// the whole text through k_xdec_slow, which writes pair order instead.
+__global__ __launch_bounds__(kDecBlock) void k_xdec_span(Text text, uint64_t* cnt, uint4* smag,
+                                                     uint8_t* sneg) {
+  __shared__ uint4 win4[kWin / 16 + 1];
+  __shared__ uint16_t pos[kXSpanSlots];  // colon, relative to b0
+  __shared__ int sfail;
+  if (threadIdx.x == 0) sfail = 0;
+  const size_t span = blockIdx.x, b0 = span * kDecSpan;
+  const long long w0 = (long long)b0 - kWinPad;
+  if (w0 >= (long long)text.mis && w0 + 16LL * (kWin / 16 + 1) <= (long long)text.L) {
+    const u32x4* a = reinterpret_cast<const u32x4*>(text.al + w0);
+    const int c2 = min((int)threadIdx.x + 2 * kDecBlock, kWin / 16);
+    const u32x4 v0 = __builtin_nontemporal_load(a + threadIdx.x),
+                v1 = __builtin_nontemporal_load(a + threadIdx.x + kDecBlock), v2 = __builtin_nontemporal_load(a + c2);
+    win4[threadIdx.x] = make_uint4(v0.x, v0.y, v0.z, v0.w);
+    win4[threadIdx.x + kDecBlock] = make_uint4(v1.x, v1.y, v1.z, v1.w);
+    if ((int)threadIdx.x + 2 * kDecBlock <= kWin / 16) win4[c2] = make_uint4(v2.x, v2.y, v2.z, v2.w);
+  } else {
+    for (int c = threadIdx.x; c < kWin / 16 + 1; c += kDecBlock) win4[c] = text.chunk(w0 + 16LL * c);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    size_t a = t.mis;
-    while (a < t.L && is_ws(t[a])) ++a;
-    size_t z = t.L;
-    while (z > t.mis && is_ws(t[z - 1])) --z;
-    if (a >= t.L || t[a] != '[') atomicMin(bad, (unsigned long long)(a - t.mis));
-    else if (z <= a + 1 || t[z - 1] != ']') atomicMin(bad, (unsigned long long)(z > t.mis ? z - 1 - t.mis : 0));
-    else if (stotal != nvals) atomicMin(bad, (unsigned long long)(t.L - t.mis));
-    az[0] = a + 1;
-    az[1] = z > t.mis ? z - 1 : t.mis;
-  }
+  const int lo = kWinPad + kDecBytes * threadIdx.x;
+  const uint4 c0 = win4[lo / 16], c1 = win4[lo / 16 + 1];
+  const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  uint32_t m = colons32(w);
+  uint32_t total;
+  const uint32_t first = block_excl_scan32(__popc(m), &total);
+  for (int k = (int)first; m && k < kXSpanSlots; m &= m - 1, ++k)
+    pos[k] = (uint16_t)(kDecBytes * threadIdx.x + __ffs(m) - 1);
   __syncthreads();
-  if (nvals == 0)
-    for (size_t i = az[0] + threadIdx.x; i < az[1]; i += blockDim.x)
-      if (!is_ws(t[i])) atomicMin(bad, (unsigned long long)(i - t.mis));
+  const size_t len = text.L - text.mis;
+  // span 0 holds the text's first colon (virtual offset <= 20) unless the
+  // text is not compact
+  bool fail = total > (uint32_t)kXSpanSlots || (span == 0 && total == 0 && len > 0);
+  const uint32_t nloc = min(total, (uint32_t)kXSpanSlots);
+  const uint32_t* l32 = reinterpret_cast<const uint32_t*>(win4);
+  uint4* dst = smag + span * kXSpanSlots;
+  uint8_t* dneg = sneg + span * kXSpanSlots;
+  for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
+    const uint32_t at = pos[idx];
+    FastNum fn;
+    const uint32_t f = fast_value(l32, at + 1 + kWinPad, b0 + at + 1 - text.mis, len, fn);
+    if ((f & SEG_OK) && (span != 0 || idx != 0 || (f & SEG_FIRST))) {
+      xst16(dst + idx, make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]));
+      dneg[idx] = (uint8_t)((fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0) | ((fn.key == 'b') << 1));
+    } else {
+      fail = true;
+    }
+  }
+  if (__ballot(fail) != 0 && __lane_id() == 0) sfail = 1;  // (__syncthreads_or costs 4 KiB of LDS)
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[span] = total | (sfail ? kWsBit : 0);
 }
 
 unsigned blocks_of(size_t n, size_t per) { return (unsigned)((n + per - 1) / per); }
 
 // exclusive scan of x[0..n) in place, x[n] = total; bsum: blocks_of(n)+1 scratch
-hipError_t scan_u64(uint64_t* x, size_t n, uint64_t* bsum, LaunchCfg c) {
+hipError_t scan_u64(uint64_t* x, size_t n, uint64_t* bsum, LaunchCfg c, uint4* map = nullptr,
+                    size_t nmap = 0) {
   const unsigned nb = blocks_of(n, kScanBlock);
   if (nb <= 1) {
-    AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c, x, n);
+    AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c, x, n, map, nmap);
     return hipGetLastError();
   }
   LaunchCfg c0 = c, c1 = c, c2 = c;
@@ -1075,8 +1222,8 @@ hipError_t scan_u64(uint64_t* x, size_t n, uint64_t* bsum, LaunchCfg c) {
   c1.ev_start = c1.ev_stop = nullptr;
   c2.ev_start = nullptr;
   AMPH_LAUNCH(k_scan_reduce, dim3(nb), dim3(kScanBlock), c0, x, n, bsum);
-  AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c1, bsum, (size_t)nb);
-  AMPH_LAUNCH(k_scan_apply, dim3(nb), dim3(kScanBlock), c2, x, n, bsum, (size_t)nb);
+  AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c1, bsum, (size_t)nb, (uint4*)nullptr, (size_t)0);
+  AMPH_LAUNCH(k_scan_apply, dim3(nb), dim3(kScanBlock), c2, x, n, bsum, (size_t)nb, map, nmap);
   return hipGetLastError();
 }
 
@@ -1107,7 +1254,7 @@ hipError_t launch_exchange_encode(const uint4* mag, const uint8_t* neg, size_t n
     hipError_t e = scan_u64(bs, nb, tmp, cm);
     if (e != hipSuccess) return e;
   } else {
-    AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c0, bs, (size_t)0);
+    AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c0, bs, (size_t)0, (uint4*)nullptr, (size_t)0);
   }
   AMPH_LAUNCH(k_xenc_write, dim3(nb ? (unsigned)nb : 1u), dim3(kXBlock), c1, mag, neg, npairs, bs,
               nb, out, out_len);
@@ -1129,7 +1276,7 @@ hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, u
   c0.ev_stop = nullptr;
   cm.ev_start = cm.ev_stop = nullptr;
   c1.ev_start = nullptr;
-  // count, scan, compact pass, general pass, check
+  // count, scan, compact pass, general pass (+ the array check)
   uint64_t* bscan = static_cast<uint64_t*>(scratch);
   uint64_t* bsum = bscan + nb + 1;
   unsigned int* slow = reinterpret_cast<unsigned int*>(bsum + blocks_of(nb, kScanBlock) + 1);
@@ -1138,9 +1285,38 @@ hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, u
   if (e != hipSuccess) return e;
   AMPH_LAUNCH(k_xdec_fast, dim3((unsigned)nb), dim3(kDecBlock), cm, t, bscan, nb, 2 * npairs, mag, neg,
               slow);
-  AMPH_LAUNCH(k_xdec_slow<ScanBases>, dim3((unsigned)std::min<size_t>(nb, kSlowGrid)), dim3(kDecBlock), cm, t,
+  AMPH_LAUNCH(k_xdec_slow<ScanBases>, dim3((unsigned)std::min<size_t>(nb, kSlowGrid)), dim3(kDecBlock), c1, t,
               ScanBases{bscan, nb}, nb, 2 * npairs, mag, neg, bad, (const unsigned int*)slow);
-  AMPH_LAUNCH(k_xdec_check<ScanTotal>, dim3(1), dim3(256), c1, t, ScanTotal{bscan, nb}, 2 * npairs, bad);
+  return hipGetLastError();
+}
+
+static_assert(kDecSpan == kXSpanBytes, "span form: one decode workgroup per span");
+
+size_t xspan_spans(size_t len) { return blocks_of(len + 16, kDecSpan); }
+size_t xspan_slots(size_t len, size_t npairs) {
+  return std::max(xspan_spans(len) * (size_t)kXSpanSlots, 2 * npairs);
+}
+size_t xspan_map_words(size_t npairs) { return blocks_of(2 * npairs, kXMapValues) + 1; }
+size_t xdec_spans_scratch_bytes(size_t len) { return 8 * ((size_t)blocks_of(xspan_spans(len), kScanBlock) + 1); }
+
+// the span pass, the scan of its count words (+ the map), the general pass
+// (+ the array check; returns at once unless a span failed or the count is off)
+hipError_t launch_exchange_decode_spans(const char* text, size_t len, size_t npairs, const XSpans& out,
+                                        unsigned long long* bad, void* scratch, const LaunchCfg& c) {
+  const size_t mis = (uintptr_t)text & 15;
+  const Text t{reinterpret_cast<const uint8_t*>(text) - mis, mis, mis + len};
+  const size_t nb = blocks_of(t.L ? t.L : 1, kDecSpan);
+  if (nb != out.nb) return hipErrorInvalidValue;
+  LaunchCfg c0 = c, cm = c, c1 = c;
+  c0.ev_stop = nullptr;
+  cm.ev_start = cm.ev_stop = nullptr;
+  c1.ev_start = nullptr;
+  AMPH_LAUNCH(k_xdec_span, dim3((unsigned)nb), dim3(kDecBlock), c0, t, out.base, out.mag, out.neg);
+  hipError_t e = scan_u64(out.base, nb, static_cast<uint64_t*>(scratch), cm, out.map, xspan_map_words(npairs));
+  if (e != hipSuccess) return e;
+  AMPH_LAUNCH(k_xdec_slow<SpanBases>, dim3((unsigned)std::min<size_t>(nb, kSlowGrid)), dim3(kDecBlock), c1, t,
+              (SpanBases{out.base, nb, 2 * npairs, out.map}), nb, 2 * npairs, out.mag, out.neg, bad,
+              (const unsigned int*)nullptr);
   return hipGetLastError();
 }
 

@@ -364,6 +364,53 @@ __global__ __launch_bounds__(kPairBlock) void k_odo_post(const uint4* opened,
 // at N = 3).  Each party's diff pair (2 x 16 B) is one 32-B-strided lane
 // access; STAGE_MAG instead brings the workgroup's run of them in through LDS
 // like the triples (tools/ubench/ubench_open_post.hip measures both).
+// Pair k's two diffs from a party in the exchange decode's span form
+// (XSpans).  The workgroup's 256 values (kXMapValues) lie in spans s0, s0 + 1,
+// s0 + 2 (a full span holds >= 167 values: a value's text is at most 49
+// bytes); span_win reads the total and the workgroup's map window (s0 and
+// the three span boundaries inside it, completed by the decode) as two
+// independent uniform loads, issued before the triples are staged so their
+// latency hides under the staging; span_slot then places each value by three
+// compares (a loop over further bases only if a span were shorter).  In text
+// order a pair may list "b" first (bit 1 of its byte): d, e are swapped back.
+// When the general pass ran (fail bits in base[nb], or a count other than
+// 2 pairs) the values sit in pair order, slot = index.
+static_assert(kXMapValues == 2 * kPairBlock, "one map entry per k_open_post workgroup");
+struct SpanWin {
+  uint4 e;  // the workgroup's map window
+  bool pair_order;
+};
+
+__device__ __forceinline__ void span_win(const uint64_t* base, const uint4* map, size_t nb, size_t pairs,
+                                         SpanWin& w) {
+  w.pair_order = base[nb] != 2 * pairs;
+  w.e = map[blockIdx.x];  // (not used in pair order)
+}
+
+// slot of value v (in this workgroup's window)
+__device__ __forceinline__ size_t span_slot(const SpanWin& w, const uint64_t* base, size_t nb, size_t v) {
+  if (w.pair_order) return v;
+  const size_t t = v - (size_t)blockIdx.x * kXMapValues, s0 = w.e.x;
+  const uint32_t o1 = w.e.z & 0xFFFFu, o2 = w.e.z >> 16;
+  if (t < o1) return s0 * kXSpanSlots + w.e.y + t;
+  if (t < o2) return (s0 + 1) * kXSpanSlots + (t - o1);
+  if (t < w.e.w) return (s0 + 2) * kXSpanSlots + (t - o2);
+  size_t s = s0 + 3;
+  while (s < nb && base[s + 1] <= v) ++s;
+  return s * kXSpanSlots + (v - base[s]);
+}
+
+__device__ __forceinline__ void span_pair(const uint4* mag, const uint8_t* negb, const uint64_t* base, size_t nb,
+                                          const SpanWin& w, size_t k, uint4& md, uint4& me, uint32_t& sg) {
+  const size_t a = span_slot(w, base, nb, 2 * k), b = span_slot(w, base, nb, 2 * k + 1);
+  const uint4 x = ld(mag + a), y = ld(mag + b);
+  const uint32_t nx = negb[a], ny = negb[b];
+  const bool swap = (nx & 2u) != 0;
+  md = swap ? y : x;
+  me = swap ? x : y;
+  sg = swap ? ((ny & 1u) | ((nx & 1u) << 8)) : ((nx & 1u) | ((ny & 1u) << 8));
+}
+
 template <int NP, bool BIG, bool STAGE_MAG>
 __global__ __launch_bounds__(kPairBlock) void k_open_post(SignedSet d, int n, const uint4* triples,
                                                          size_t pairs, int p0, uint4* ow, uint4* ou,
@@ -374,6 +421,12 @@ __global__ __launch_bounds__(kPairBlock) void k_open_post(SignedSet d, int n, co
   const size_t k0 = (size_t)blockIdx.x * kPairBlock;
   const size_t k = k0 + threadIdx.x;
   const size_t nblk = min((size_t)kPairBlock, pairs - k0);
+  SpanWin sw[NP > 0 ? NP : 1];
+  if constexpr (NP > 0) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+      if (!STAGE_MAG && d.sbase[j]) span_win(d.sbase[j], d.smap[j], d.snb[j], pairs, sw[j]);
+  }
   stage_tuples<6, kPairBlock>(tri, triples + 6 * k0, nblk);
   W4 D = {}, E = {};
   if constexpr (NP > 0) {
@@ -386,6 +439,14 @@ __global__ __launch_bounds__(kPairBlock) void k_open_post(SignedSet d, int n, co
     }
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
+      if (!STAGE_MAG && d.sbase[j]) {  // a partner's decoded text in span form
+        md[j] = me[j] = make_uint4(0, 0, 0, 0);
+        sg[j] = 0;
+        if (k < pairs)
+          span_pair(d.mag[j], reinterpret_cast<const uint8_t*>(d.neg[j]), d.sbase[j], d.snb[j], sw[j], k, md[j],
+                    me[j], sg[j]);
+        continue;
+      }
       if constexpr (!STAGE_MAG) {
         md[j] = k < pairs ? ld(d.mag[j] + 2 * k) : make_uint4(0, 0, 0, 0);
         me[j] = k < pairs ? ld(d.mag[j] + 2 * k + 1) : make_uint4(0, 0, 0, 0);
@@ -408,8 +469,18 @@ __global__ __launch_bounds__(kPairBlock) void k_open_post(SignedSet d, int n, co
     __syncthreads();
     if (k >= pairs) return;
     for (int j = 0; j < n; ++j) {
-      const uint32_t s = reinterpret_cast<const uint16_t*>(d.neg[j])[k];
-      const W4 x = canon<BIG>(w4(ld(d.mag[j] + 2 * k)), f), y = canon<BIG>(w4(ld(d.mag[j] + 2 * k + 1)), f);
+      uint4 mx, my;
+      uint32_t s;
+      if (d.sbase[j]) {
+        SpanWin w;
+        span_win(d.sbase[j], d.smap[j], d.snb[j], pairs, w);
+        span_pair(d.mag[j], reinterpret_cast<const uint8_t*>(d.neg[j]), d.sbase[j], d.snb[j], w, k, mx, my, s);
+      } else {
+        s = reinterpret_cast<const uint16_t*>(d.neg[j])[k];
+        mx = ld(d.mag[j] + 2 * k);
+        my = ld(d.mag[j] + 2 * k + 1);
+      }
+      const W4 x = canon<BIG>(w4(mx), f), y = canon<BIG>(w4(my), f);
       D = (s & 0xFF) ? mod_sub(D, x, f) : mod_add(D, x, f);
       E = (s >> 8) ? mod_sub(E, y, f) : mod_add(E, y, f);
     }
@@ -876,6 +947,8 @@ hipError_t launch_odo_pre(const uint4* share_data, int stride_w, const uint4* ma
 
 hipError_t launch_open_diffs(const SignedSet& d, int n, size_t words, uint4* out, const Fp& f,
                              const LaunchCfg& c) {
+  for (int j = 0; j < n; ++j)
+    if (d.sbase[j]) return hipErrorInvalidValue;  // span form: k_open_post only
   if (words == 0) return hipSuccess;
   const size_t nvals = 4 * words;
   const unsigned g = grid_for(nvals, c);
@@ -897,6 +970,8 @@ hipError_t launch_odo_post(const uint4* opened, const uint4* triples, size_t wor
 
 hipError_t launch_open_post(const SignedSet& d, int n, const uint4* triples, size_t words, int p0,
                             uint4* ow, uint4* ou, const Fp& f, const LaunchCfg& c, bool stage_mag) {
+  for (int j = 0; j < n && stage_mag; ++j)
+    if (d.sbase[j]) return hipErrorInvalidValue;  // span form: direct loads only
   if (words == 0) return hipSuccess;
   const size_t pairs = 2 * words;
   const dim3 g((unsigned)((pairs + kPairBlock - 1) / kPairBlock));

@@ -23,9 +23,36 @@ struct ShareSet {
   const uint4* s[kMaxParties];
 };
 
+// The exchange decode's SPAN FORM (launch_exchange_decode_spans): the values
+// of 8 KiB span s of the text, in text order, at slots [kXSpanSlots s, ...);
+// neg byte per slot = sign (bit 0) | key "b" (bit 1).  base[s] = the index of
+// span s's first value (bits 0..39), base[nb] = the total; when base[nb]
+// carries bits above 39 or its count is not the pair count x 2, the general
+// pass wrote the values in pair order instead (slot = value index).  map[b]
+// = the window of values [kXMapValues b, kXMapValues (b + 1)) (one
+// k_open_post workgroup's): x = s0, the span holding its first value, y = that
+// value's rank in s0, z = o1 | o2 << 16, w = o3 with o_i = base[s0 + i] -
+// kXMapValues b (0xFFFF / ~0 past the last span): value kXMapValues b + t
+// lies in span s0 + i for o_i <= t < o_(i+1) (o_0 = -y).
+constexpr size_t kXSpanBytes = 8192;
+constexpr int kXSpanSlots = 528;  // 33 x 256 B per span: not a power-of-two stride (see k_xdec_span)
+constexpr size_t kXMapValues = 256;
+struct XSpans {
+  uint4* mag;
+  uint8_t* neg;
+  uint64_t* base;  // nb + 1 words
+  uint4* map;      // xspan_map_words(npairs) windows
+  size_t nb;       // xspan_spans(len)
+};
+
 struct SignedSet {  // per party: diff magnitudes (2 words per pair) + sign words
   const uint4* mag[kMaxParties];
   const uint32_t* neg[kMaxParties];  // 4 sign bytes per source word (see K_ODO_PRE)
+  // span form (k_open_post only): base / map / nb of the party's XSpans, null
+  // for pair-ordered diffs (amph_odo_pre's layout)
+  const uint64_t* sbase[kMaxParties];
+  const uint4* smap[kMaxParties];
+  size_t snb[kMaxParties];
 };
 
 struct TextSet {  // base64 text of each ODO field: t[field][party], 16-byte aligned
@@ -111,6 +138,13 @@ size_t xdec_scratch_bytes(size_t len);
 hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, uint4* mag,
                                   uint8_t* neg, unsigned long long* bad, void* scratch,
                                   const LaunchCfg& c);
+// decode into span form (see XSpans): one read of the text, no count pass
+size_t xspan_spans(size_t len);
+size_t xspan_slots(size_t len, size_t npairs);  // >= both the span slots and 2 npairs
+size_t xspan_map_words(size_t npairs);
+size_t xdec_spans_scratch_bytes(size_t len);
+hipError_t launch_exchange_decode_spans(const char* text, size_t len, size_t npairs, const XSpans& out,
+                                        unsigned long long* bad, void* scratch, const LaunchCfg& c);
 
 // Synthetic honest n-party ODOs (bench/test input generator, device-side).
 struct OutSet {

@@ -373,10 +373,14 @@ int amph_exchange_decode(amph_ctx* ctx, const char* text, size_t len, size_t npa
  * Only the texts and the ODO fields cross PCIe: the triples, the diffs and the
  * opened values never leave the GPU (a host-path amph_odo_pre / exchange /
  * amph_open_post sequence moves them both ways).  Results are bit-identical to
- * that sequence.  A session belongs to one context (calls are serialised by
- * its mutex), holds 456 + 68 n_parties bytes per word of device memory (the
- * triples, five fields, every party's diffs, its own text at most) plus one
- * partner text at a time until amph_party_free, and may be finished once.
+ * that sequence.  A partner's text is decoded in one read (the values of each
+ * 8 KiB of text in their own slots, found by finish through the decoded span
+ * bases; no count pass), where amph_exchange_decode reads its text twice to
+ * write pair order.  A session belongs to one context (calls are serialised by
+ * its mutex), holds 524 bytes per word of device memory (the triples, five
+ * fields, its own diffs and text at most) plus about 1.07 x each partner
+ * text's length (that partner's diffs) and one partner text at a time until
+ * amph_party_free, and may be finished once.
  * amph_party_words = the session's word count; free sessions before their
  * context.  Status semantics
  * as the calls it replaces (amph_exchange_decode's AMPH_E_PARAM / AMPH_E_LEN
@@ -394,6 +398,31 @@ int amph_party_finish(amph_party* party, int is_player0, uint8_t* out_w, uint8_t
  * 4 * ceil(16 * words / 3) characters each, no terminator */
 int amph_party_finish_b64(amph_party* party, int is_player0, char* const fields_b64[5]);
 void amph_party_free(amph_party* party);
+
+/* The same session on device buffers, for a server whose tuples and texts are
+ * already in GPU memory (e.g. received by RDMA into device memory): nothing is
+ * copied to or from the host and nothing synchronises the host; every call
+ * is asynchronous on `stream` (one stream per session; amph_party_free waits
+ * for it).  begin: share_data, mask_tuples, triples are 16-byte aligned device
+ * buffers used in place -- the triples must stay unchanged until finish --
+ * and out_y / out_r / out_v (optional) device outputs, which then also hold
+ * the session's copies of those fields until finish.  text_dev: the device
+ * addresses of this party's text and of its length (a device uint64_t), valid
+ * once the stream has run begin; the text's capacity is
+ * amph_exchange_max_chars(2 * words).  partner_dev: text is device memory of
+ * the given length; *bad_index is a device word set as amph_exchange_decode's
+ * device mode sets it (AMPH_NO_FAILURE when the text held) -- check it before
+ * finishing.  finish_b64_dev: the five fields as base64 into device buffers
+ * (amph_party_finish_b64's lengths).  A device-mode session takes only these
+ * calls (and amph_party_words / amph_party_free); a multi-device context is
+ * refused. */
+int amph_party_begin_dev(amph_ctx* ctx, const uint8_t* share_data, size_t share_stride,
+                         const uint8_t* mask_tuples, const uint8_t* triples, size_t words, int n_parties,
+                         uint8_t* out_y, uint8_t* out_r, uint8_t* out_v, void* stream, amph_party** out);
+int amph_party_text_dev(amph_party* party, const char** text, const uint64_t** text_len);
+int amph_party_partner_dev(amph_party* party, int slot, const char* text, size_t len, int64_t* bad_index,
+                           void* stream);
+int amph_party_finish_b64_dev(amph_party* party, int is_player0, char* const fields_b64[5], void* stream);
 
 /* ---- benchmark / test input generation (device pointers only) ---------- */
 /* Honest n-party ODOs: out_fields[k * n_parties + j] = field k (y,r,v,w,u) of

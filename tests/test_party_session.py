@@ -138,3 +138,123 @@ def test_session_empty(ctx):
     w, u = s.finish(False)
     assert w.shape == (0, 16) and u.shape == (0, 16)
     s.close()
+
+
+def reorder_text(t: bytes) -> bytes:
+    """The same FactorPairs with "b" listed before "a" (a JSON reader accepts
+    either member order; the span-form decode keeps text order and k_open_post
+    swaps the pair back by its key bit)."""
+    import re
+    return re.sub(rb'\{"a":(-?\d+),"b":(-?\d+)\}', rb'{"b":\2,"a":\1}', t)
+
+
+def test_session_partner_text_forms(ctx, F):
+    """Every partner text form decodes to the same diffs: Jackson's compact
+    text (span form), members swapped (span form, swapped back by finish),
+    whitespace between tokens (the general pass: pair order), and a mix of
+    partners in both forms in one finish."""
+    n, W = 3, 20000
+    shares, masks, triples = party_inputs(F, n, W)
+    pre = [F.odo_pre(shares[j], 32, masks[j], triples[j]) for j in range(n)]
+    texts = [ctx.party_begin(shares[j], 32, masks[j], triples[j], n).text() for j in range(1, n)]
+    opened = F.recombine_diffs([p[3] for p in pre], [p[4] for p in pre])
+    ow, ou = F.odo_post(opened, triples[0], True)
+    forms = {
+        "compact": texts,
+        "swapped": [reorder_text(t) for t in texts],
+        "spaced": [t.replace(b',"b"', b', "b"').replace(b"},{", b"},\n{") for t in texts],
+        "mixed": [reorder_text(texts[0]), texts[1].replace(b":", b": ")],
+    }
+    for name, ts in forms.items():
+        s = ctx.party_begin(shares[0], 32, masks[0], triples[0], n, want_yrv=False)
+        for slot, t in enumerate(ts, start=1):
+            s.partner(slot, t)
+        w, u = s.finish(True)
+        assert np.array_equal(w, ow) and np.array_equal(u, ou), name
+        s.close()
+
+
+def test_session_small_diffs(ctx, F):
+    """Triples whose a, b equal the words they are subtracted from: every diff
+    is 0, the texts are {"a":0,"b":0} runs (over 1000 values per 8 KiB, more
+    than a span's slots: the general pass decodes them), and the products are
+    the c shares (+ nothing): checked against the oracle."""
+    n, W = 2, 9000
+    shares, masks, triples = party_inputs(F, n, W)
+    for j in range(n):
+        t = triples[j].copy()
+        t[0::2, 0:16] = shares[j][:, 0:16]
+        t[0::2, 32:48] = masks[j][0::2, 0:16]
+        t[1::2, 0:16] = masks[j][1::2, 0:16]
+        t[1::2, 32:48] = masks[j][0::2, 0:16]
+        triples[j] = t
+    pre = [F.odo_pre(shares[j], 32, masks[j], triples[j]) for j in range(n)]
+    assert not pre[0][3].any()
+    s0 = ctx.party_begin(shares[0], 32, masks[0], triples[0], n)
+    s1 = ctx.party_begin(shares[1], 32, masks[1], triples[1], n)
+    t1 = s1.text()
+    assert t1.startswith(b'[{"a":0,"b":0},{"a":0,"b":0}')
+    s0.partner(1, t1)
+    w, u = s0.finish(True)
+    opened = F.recombine_diffs([p[3] for p in pre], [p[4] for p in pre])
+    ow, ou = F.odo_post(opened, triples[0], True)
+    assert np.array_equal(w, ow) and np.array_equal(u, ou)
+    s0.close()
+    s1.close()
+
+
+@pytest.mark.parametrize("n,W,stride", [(3, 5000, 32), (2, 70001, 16)])
+def test_session_device_mode(ctx, F, n, W, stride):
+    """amph_party_*_dev on torch device tensors, texts handed between the
+    parties on the device: the five base64 fields equal the host session's /
+    the oracle's."""
+    import torch
+    shares, masks, triples = party_inputs(F, n, W, stride)
+    pre = [F.odo_pre(shares[j], stride, masks[j], triples[j]) for j in range(n)]
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    inputs = [(dev(shares[j]), dev(masks[j]), dev(triples[j])) for j in range(n)]
+    sessions = [ctx.party_begin_dev(*inputs[j][:1], stride, *inputs[j][1:], n) for j in range(n)]
+    texts = []
+    for j, s in enumerate(sessions):
+        t, ln = s.text_dev()
+        texts.append((t, ln))
+        if j == 0 and W <= 5000:
+            assert s.text() == jackson_text(pre[0][3], pre[0][4])
+    lens = [int(ln.item()) for _, ln in texts]
+    for j, s in enumerate(sessions):
+        others = [k for k in range(n) if k != j]
+        bads = [s.partner(slot, texts[k][0][:lens[k]]) for slot, k in enumerate(others, start=1)]
+        fields = s.finish_b64(j == 0)
+        torch.cuda.synchronize()
+        assert all(int(b.item()) == 0x7F7F7F7F7F7F7F7F for b in bads)
+        opened = F.recombine_diffs([pre[k][3] for k in [j] + others], [pre[k][4] for k in [j] + others])
+        ow, ou = F.odo_post(opened, triples[j], j == 0)
+        want = [base64.b64encode(x.tobytes()) for x in (pre[j][0], pre[j][1], pre[j][2], ow, ou)]
+        assert [f.cpu().numpy().tobytes() for f in fields] == want
+    for s in sessions:
+        s.close()
+
+
+def test_session_device_mode_errors(ctx, F):
+    """A malformed partner text is reported in the device word; host calls on a
+    device-mode session (and the reverse) are refused."""
+    import torch
+    import amphora_amd as A
+    n, W = 2, 3000
+    shares, masks, triples = party_inputs(F, n, W)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    s = ctx.party_begin_dev(dev(shares[0]), 32, dev(masks[0]), dev(triples[0]), n)
+    t1 = ctx.party_begin(shares[1], 32, masks[1], triples[1], n).text()
+    at = t1.index(b":") + 3
+    bad_text = t1[:at] + b"x" + t1[at + 1:]
+    bad = s.partner(1, dev(np.frombuffer(bad_text, np.uint8)))
+    assert 6 <= int(bad.item()) <= at
+    with pytest.raises(A.AmphoraNativeError, match="takes the \\*_dev calls"):
+        A._lib.PartySession.finish(s, True)
+    h = ctx.party_begin(shares[1], 32, masks[1], triples[1], n)
+    import ctypes as C
+    t, ln = C.c_void_p(), C.c_void_p()
+    assert A._lib.lib.amph_party_text_dev(h._h, C.byref(t), C.byref(ln)) == A._lib.AMPH_E_PARAM
+    assert b"host-mode party session takes the host calls" in A._lib.lib.amph_last_error()
+    s.close()
+    h.close()

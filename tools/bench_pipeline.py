@@ -4,7 +4,9 @@
   OutputDeliveryService.java:75-286, + the VerifiableSecretShare response):
   K_ODO_PRE -> own MultiplicationExchangeObject array text (exchange encode)
   -> the N-1 partners' texts parsed (exchange decode) -> open + K_ODO_POST
-  (k_open_post) -> base64 of the five ODO fields;
+  (k_open_post) -> base64 of the five ODO fields; once through the per-call
+  device API (pair-order decode) and once as a device-mode party session
+  (amph_party_*_dev: one-read span-form decode);
 * client download (DefaultAmphoraClient.getSecret, :206-217): base64 decode of
   the N parties' five ODO fields -> K_RV;
 * client upload (createSecret, :150-170): base64 decode of the N mask ODOs ->
@@ -91,6 +93,23 @@ def party(mark):
     mark("base64_encode_x5")
 
 
+def party_session(mark):
+    """The same Output Delivery as a device-mode party session
+    (amph_party_*_dev): partner texts decoded in one read into span form,
+    finish reading them through the span bases."""
+    s = ctx.party_begin_dev(share, 32, masks, triples, n)
+    mark("begin (k_odo_pre + encode)")
+    t, ln = s.text_dev()
+    L = int(ln.item())  # the body length a server needs to send it
+    mark("text length read back")
+    for slot in range(1, n):
+        s.partner(slot, t[:L])
+    mark("partners x%d (decode to span form)" % (n - 1))
+    s.finish_b64(False)
+    mark("finish_b64 (k_open_post + base64 x5)")
+    s.close()
+
+
 def download(mark):
     fields = [tuple(ctx.base64_decode(t)[0].view(W, 16) for t in o) for o in b64_odos]
     mark("base64_decode_x%d" % (5 * n))
@@ -118,6 +137,7 @@ def upload_fused(mark):
 
 
 out = {"words": W, "parties": n, "party_output_delivery": stages(party),
+       "party_output_delivery_session": stages(party_session),
        "client_download": stages(download), "client_upload": stages(upload),
        "client_download_fused": stages(download_fused), "client_upload_fused": stages(upload_fused)}
 print(json.dumps(out))

@@ -27,6 +27,31 @@ __global__ void k_fill(uint4* mag, uint8_t* neg, size_t nvals, int full) {
   }
 }
 
+// span form -> pair order (what k_open_post reads through its map window)
+__global__ void k_unspan(XSpans x, size_t npairs, uint4* mag, uint8_t* neg) {
+  const size_t k = (size_t)blockIdx.x * 128 + threadIdx.x;
+  if (k >= npairs) return;
+  const uint64_t tot = x.base[x.nb];
+  const uint4 e = x.map[blockIdx.x];
+  size_t sl[2];
+  for (int h = 0; h < 2; ++h) {
+    const size_t v = 2 * k + h, t = v - (size_t)blockIdx.x * 256;
+    const uint32_t o1 = e.z & 0xFFFF, o2 = e.z >> 16;
+    sl[h] = tot != 2 * npairs ? v
+            : t < o1        ? (size_t)e.x * kXSpanSlots + e.y + t
+            : t < o2        ? (size_t)(e.x + 1) * kXSpanSlots + t - o1
+            : t < e.w       ? (size_t)(e.x + 2) * kXSpanSlots + t - o2
+                            : ~(size_t)0;
+  }
+  if (sl[0] == ~(size_t)0 || sl[1] == ~(size_t)0) { neg[2 * k] = 0xEE; return; }  // (counted as mismatches)
+  const size_t a = sl[0], b = sl[1];
+  const bool sw = (x.neg[a] & 2) != 0;
+  mag[2 * k] = sw ? x.mag[b] : x.mag[a];
+  mag[2 * k + 1] = sw ? x.mag[a] : x.mag[b];
+  neg[2 * k] = (sw ? x.neg[b] : x.neg[a]) & 1;
+  neg[2 * k + 1] = (sw ? x.neg[a] : x.neg[b]) & 1;
+}
+
 int main(int argc, char** argv) {
   const int R = argc > 1 ? atoi(argv[1]) : 20;
   const int full = argc > 2 ? atoi(argv[2]) : 0;  // 1: full-length magnitudes (752 MB of text)
@@ -100,6 +125,45 @@ int main(int argc, char** argv) {
   printf("bad=%llx magnitudes %s, sign mismatches %zu\n", hb, a == b ? "identical" : "DIFFER", signs_bad);
   printf("decode median %8.1f us  min %8.1f us  %6.2f TB/s of text\n", ts[ts.size() / 2] * 1e3, ts[0] * 1e3,
          L / (ts[ts.size() / 2] * 1e-3) / 1e12);
+  {  // the span form (one read of the text; the party session's partner decode)
+    XSpans x{};
+    x.nb = xspan_spans(L);
+    const size_t slots = xspan_slots(L, npairs);
+    CK(hipMalloc(&x.mag, slots * 16)); CK(hipMalloc(&x.neg, slots));
+    CK(hipMalloc(&x.base, 8 * (x.nb + 1))); CK(hipMalloc(&x.map, 16 * xspan_map_words(npairs)));
+    void* s3;
+    CK(hipMalloc(&s3, xdec_spans_scratch_bytes(L)));
+    std::vector<float> tsp;
+    for (int r = 0; r < R + 3; ++r) {
+      CK(hipMemset(bad, 0x7F, 8));
+      CK(hipEventRecord(e0, 0));
+      CK(launch_exchange_decode_spans(text, L, npairs, x, bad, s3, c));
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      if (r >= 3) tsp.push_back(ms);
+    }
+    CK(hipMemset(mag2, 0, nvals * 16)); CK(hipMemset(neg2, 0, nvals));
+    hipLaunchKernelGGL(k_unspan, dim3((unsigned)((npairs + 127) / 128)), dim3(128), 0, 0, x, npairs, mag2, neg2);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(b.data(), mag2, nvals * 16, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(nb.data(), neg2, nvals, hipMemcpyDeviceToHost));
+    unsigned long long hb2, tot;
+    CK(hipMemcpy(&hb2, bad, 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(&tot, x.base + x.nb, 8, hipMemcpyDeviceToHost));
+    size_t sb = 0;
+    for (size_t i = 0; i < nvals; ++i) {
+      bool zero = true;
+      for (int k = 0; k < 16; ++k) zero = zero && a[16 * i + k] == 0;
+      if ((zero ? 0 : na[i]) != nb[i]) ++sb;
+    }
+    std::sort(tsp.begin(), tsp.end());
+    printf("spans: bad=%llx total=%llx (%s) magnitudes %s, sign mismatches %zu\n", hb2, tot,
+           tot == nvals ? "span form" : "pair order", a == b ? "identical" : "DIFFER", sb);
+    printf("decode_spans median %8.1f us  min %8.1f us  %6.2f TB/s of text\n", tsp[tsp.size() / 2] * 1e3,
+           tsp[0] * 1e3, L / (tsp[tsp.size() / 2] * 1e-3) / 1e12);
+    CK(hipFree(x.mag)); CK(hipFree(x.neg)); CK(hipFree(x.base)); CK(hipFree(x.map)); CK(hipFree(s3));
+  }
   // the general pass: one '-' turned into a space (still valid JSON, one
   // value's sign flips) takes the whole text through k_xdec_slow
   std::vector<char> h(L);
