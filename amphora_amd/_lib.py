@@ -764,13 +764,11 @@ class PartySessionDev(PartySession):
     def finish(self, is_player0: bool):
         raise AmphoraNativeError(AMPH_E_PARAM, "a device-mode session finishes with finish_b64")
 
-    def finish_b64(self, is_player0: bool, out=None):
-        """-> the five fields' base64 text as uint8 device tensors (or into out)."""
-        import torch
+    def finish_b64(self, is_player0: bool):
+        """-> the five fields' base64 text: uint8 device tensors viewing the
+        session's memory (valid until close)."""
         nc = 4 * ((16 * self.words + 2) // 3)
-        dev = self._keep[0].device
-        outs = out if out is not None else [torch.empty(max(nc, 1), dtype=torch.uint8, device=dev) for _ in range(5)]
-        arr = (C.c_void_p * 5)(*[_ptr(o) for o in outs])
+        arr = (C.c_void_p * 5)()
         Context._check(lib.amph_party_finish_b64_dev(self._h, int(is_player0), arr, self._stream()))
-        return [o[:nc] for o in outs]
+        return [_dev_view(arr[k], nc, "|u1", self.ctx.device) if nc else None for k in range(5)]
 

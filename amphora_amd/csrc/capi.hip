@@ -142,6 +142,11 @@ struct amph_ctx {
   DevBuf small_ff;
   bool small_ff_dirty = true;
   std::unique_ptr<amph::CopyPool> pool;
+  // party sessions' device buffers, kept after amph_party_free for the next
+  // session: a server runs one session per request, and hipMalloc / hipFree of
+  // its gigabytes cost tens of microseconds per buffer (hipFree synchronises
+  // the device) -- best fit, at most kPartyPoolMax buffers, freed with the context
+  std::vector<DevBuf> party_pool;
 };
 
 namespace {
@@ -804,6 +809,10 @@ void amph_ctx_destroy(amph_ctx* c) {
     (void)hipEventDestroy(c->xdev_done);
   }
   c->xdev.release();
+  if (!c->party_pool.empty()) {
+    (void)use_device(c->device);
+    for (DevBuf& b : c->party_pool) b.release();
+  }
   delete c;
 }
 
@@ -1845,6 +1854,7 @@ struct amph_party {
   DevBuf mem, tmp, io;
   const uint4* triples = nullptr;
   uint4* f5[5] = {};  // y, r, v, w, u
+  char* b64[5] = {};  // the five fields as base64 text (finish_b64)
   uint4* mag[AMPH_MAX_PARTIES] = {};
   uint8_t* neg[AMPH_MAX_PARTIES] = {};
   DevBuf pbuf[AMPH_MAX_PARTIES];
@@ -1852,6 +1862,7 @@ struct amph_party {
   char* text = nullptr;
   unsigned long long* text_len_dev = nullptr;
   void* enc_scratch = nullptr;
+  uint64_t* enc_lens = nullptr;  // K_ODO_PRE's exchange text lengths, scanned by the encode
   uint64_t text_len = 0;
   uint32_t have = 0;  // bit j: party j's diffs are on the device (bit 0 after begin)
   bool finished = false;
@@ -1865,6 +1876,40 @@ struct amph_party {
 
 namespace {
 size_t b64_chars(size_t nbytes) { return 4 * ((nbytes + 2) / 3); }
+
+constexpr size_t kPartyPoolMax = 16;
+
+// (c->mu held) hand a session buffer back to the context's pool
+void pool_put(amph_ctx* c, DevBuf& b) {
+  if (!b.p) return;
+  c->party_pool.push_back(b);
+  b.p = nullptr;
+  b.cap = 0;
+  while (c->party_pool.size() > kPartyPoolMax) {  // drop the smallest
+    size_t m = 0;
+    for (size_t i = 1; i < c->party_pool.size(); ++i)
+      if (c->party_pool[i].cap < c->party_pool[m].cap) m = i;
+    c->party_pool[m].release();
+    c->party_pool.erase(c->party_pool.begin() + (long)m);
+  }
+}
+
+// (c->mu held) b holds at least `bytes`: kept, or the best-fitting pooled
+// buffer, or a new allocation
+hipError_t pool_ensure(amph_ctx* c, DevBuf& b, size_t bytes) {
+  if (bytes <= b.cap) return hipSuccess;
+  pool_put(c, b);
+  long best = -1;
+  for (size_t i = 0; i < c->party_pool.size(); ++i)
+    if (c->party_pool[i].cap >= bytes && (best < 0 || c->party_pool[i].cap < c->party_pool[(size_t)best].cap))
+      best = (long)i;
+  if (best >= 0) {
+    b = c->party_pool[(size_t)best];
+    c->party_pool.erase(c->party_pool.begin() + best);
+    return hipSuccess;
+  }
+  return b.ensure(bytes);
+}
 
 int party_check(amph_party* p) {
   if (!p || !p->c) return fail(AMPH_E_PARAM, "null party session");
@@ -1886,12 +1931,14 @@ int party_args(amph_ctx* c, size_t share_stride, int n_parties, size_t words, co
 // the session's device memory; yrv[k] non-null: field k lives in the caller's
 // device buffer (device mode), else in the session's
 int party_alloc(amph_party* p, bool copy_triples, uint8_t* const yrv[3]) {
-  const size_t W = p->W, P = 2 * W;
+  const size_t W = p->W, P = 2 * W, nc = b64_chars(16 * W);
+  const size_t nl = (P + amph::kXLenPairs - 1) / amph::kXLenPairs;
   const size_t sz[] = {copy_triples ? 192 * W : 0, 16 * W, 16 * W, 16 * W, 16 * W, 16 * W,
-                       amph::xenc_max_bytes(P), 8, amph::xenc_scratch_bytes(P), 64 * W, 4 * W};
+                       amph::xenc_max_bytes(P), 8, amph::xenc_lens_scratch_bytes(P), 64 * W, 4 * W, nc, nc, nc, nc, nc,
+                       8 * (nl + 1)};
   size_t total = 0;
   for (size_t b : sz) total += align256(b ? b : 16);
-  if (p->mem.ensure(total) != hipSuccess) return fail(AMPH_E_NOMEM, "party session device memory");
+  if (pool_ensure(p->c, p->mem, total) != hipSuccess) return fail(AMPH_E_NOMEM, "party session device memory");
   uint8_t* cur = (uint8_t*)p->mem.p;
   auto take = [&](size_t b) {
     uint8_t* q = cur;
@@ -1908,19 +1955,22 @@ int party_alloc(amph_party* p, bool copy_triples, uint8_t* const yrv[3]) {
   p->enc_scratch = take(sz[8]);
   p->mag[0] = (uint4*)take(sz[9]);
   p->neg[0] = take(sz[10]);
+  for (int k = 0; k < 5; ++k) p->b64[k] = (char*)take(sz[11 + k]);
+  p->enc_lens = (uint64_t*)take(sz[16]);
   return AMPH_OK;
 }
 
-// k_odo_pre (y, r, v + this party's diffs) and the exchange encode of the diffs
+// k_odo_pre (y, r, v + this party's diffs and their exchange text lengths)
+// and the exchange encode of the diffs
 int party_pre(amph_party* p, const uint8_t* dshare, size_t share_stride, const uint8_t* dmasks, hipStream_t s) {
   amph_ctx* c = p->c;
   const size_t W = p->W, P = 2 * W;
   hipError_t e = amph::launch_odo_pre((const uint4*)dshare, (int)(share_stride / 16), (const uint4*)dmasks,
-                                      p->triples, W, p->f5[0], p->f5[1], p->f5[2], p->mag[0],
-                                      (uint32_t*)p->neg[0], c->f, cfg(c, s, W));
+                                      p->triples, W, p->f5[0], p->f5[1], p->f5[2], p->mag[0], (uint32_t*)p->neg[0],
+                                      c->f, cfg(c, s, W), p->enc_lens);
   if (e != hipSuccess) return hip_fail(e, "k_odo_pre");
-  e = amph::launch_exchange_encode(p->mag[0], p->neg[0], P, p->text, p->text_len_dev, p->enc_scratch,
-                                   cfg(c, s, P));
+  e = amph::launch_exchange_encode_lens(p->mag[0], p->neg[0], P, p->enc_lens, p->text, p->text_len_dev,
+                                        p->enc_scratch, cfg(c, s, P));
   return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_xenc");
 }
 
@@ -1934,7 +1984,7 @@ int party_slot_check(amph_party* p, int slot, const char* text, size_t len) {
 }
 
 // a partner's text (device memory) decoded into the slot's span form; bad:
-// the device word the decode reports into (reset here)
+// the device word the decode reports into (reset by its first kernel)
 int party_decode(amph_party* p, int slot, const char* dtext, size_t len, unsigned long long* bad, hipStream_t s) {
   const size_t P = 2 * p->W;
   const size_t nb = amph::xspan_spans(len), slots = amph::xspan_slots(len, P);
@@ -1942,7 +1992,8 @@ int party_decode(amph_party* p, int slot, const char* dtext, size_t len, unsigne
                          amph::xdec_spans_scratch_bytes(len)};
   size_t xtotal = 0;
   for (size_t b : xsz) xtotal += align256(b);
-  if (p->pbuf[slot].ensure(xtotal) != hipSuccess) return fail(AMPH_E_NOMEM, "party session partner diffs");
+  if (pool_ensure(p->c, p->pbuf[slot], xtotal) != hipSuccess)
+    return fail(AMPH_E_NOMEM, "party session partner diffs");
   uint8_t* xp = (uint8_t*)p->pbuf[slot].p;
   amph::XSpans& xs = p->xs[slot];
   xs.mag = (uint4*)xp;
@@ -1953,7 +2004,6 @@ int party_decode(amph_party* p, int slot, const char* dtext, size_t len, unsigne
   xs.nb = nb;
   p->mag[slot] = xs.mag;
   p->neg[slot] = xs.neg;
-  HIP_TRY(hipMemsetAsync(bad, 0x7F, 8, s));
   hipError_t e = amph::launch_exchange_decode_spans(dtext, len, P, xs, bad, scratch, cfg(p->c, s, len));
   return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_xdec");
 }
@@ -1992,14 +2042,13 @@ int party_open_post(amph_party* p, int is_player0, hipStream_t s) {
   return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_open_post");
 }
 
-// the five fields as base64 text into out[k] (device memory)
-int party_b64(amph_party* p, char* const out[5], hipStream_t s) {
+// the five fields as base64 text in the session's memory (one launch)
+int party_b64(amph_party* p, hipStream_t s) {
   const size_t nb = 16 * p->W;
-  for (int k = 0; k < 5 && nb; ++k) {
-    hipError_t e = amph::launch_b64_encode((const uint8_t*)p->f5[k], nb, out[k], cfg(p->c, s, (nb + 11) / 12));
-    if (e != hipSuccess) return hip_fail(e, "k_b64_encode");
-  }
-  return AMPH_OK;
+  const uint8_t* const in[5] = {(const uint8_t*)p->f5[0], (const uint8_t*)p->f5[1], (const uint8_t*)p->f5[2],
+                                (const uint8_t*)p->f5[3], (const uint8_t*)p->f5[4]};
+  hipError_t e = amph::launch_b64_encode_multi(in, p->b64, 5, nb, cfg(p->c, s, (nb + 11) / 12));
+  return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_b64_encode_multi");
 }
 
 int party_mode(amph_party* p, bool dev) {
@@ -2026,7 +2075,7 @@ int amph_party_begin(amph_ctx* c, const uint8_t* share_data, size_t share_stride
   const size_t W = words;
   uint8_t* const none[3] = {nullptr, nullptr, nullptr};
   if (int st = party_alloc(p.get(), true, none)) return st;
-  if (p->tmp.ensure(align256(share_stride * W + 16) + align256(64 * W + 16)) != hipSuccess)
+  if (pool_ensure(c, p->tmp, align256(share_stride * W + 16) + align256(64 * W + 16)) != hipSuccess)
     return fail(AMPH_E_NOMEM, "party session staging");
   uint8_t* dshare = (uint8_t*)p->tmp.p;
   uint8_t* dmasks = dshare + align256(share_stride * W + 16);
@@ -2044,7 +2093,7 @@ int amph_party_begin(amph_ctx* c, const uint8_t* share_data, size_t share_stride
                         {orr, p->f5[1], orr ? 16 * W : 0}, {ov, p->f5[2], ov ? 16 * W : 0}}));
   p->text_len = len;
   p->have = 1u;
-  p->tmp.release();
+  pool_put(c, p->tmp);
   *out = p.release();
   return AMPH_OK;
 }
@@ -2076,7 +2125,8 @@ int amph_party_partner(amph_party* p, int slot, const char* text, size_t len, in
   amph_ctx* c = p->c;
   HIP_TRY(use_device(c->device));
   std::lock_guard<std::mutex> g(c->mu);
-  if (p->io.ensure(align256(len + 16) + 256) != hipSuccess) return fail(AMPH_E_NOMEM, "party session text staging");
+  if (pool_ensure(c, p->io, align256(len + 16) + 256) != hipSuccess)
+    return fail(AMPH_E_NOMEM, "party session text staging");
   uint8_t* dtext = (uint8_t*)p->io.p;
   unsigned long long* dbad = (unsigned long long*)(dtext + align256(len + 16));
   hipStream_t s;
@@ -2115,16 +2165,14 @@ int amph_party_finish_b64(amph_party* p, int is_player0, char* const fields_b64[
   amph_ctx* c = p->c;
   HIP_TRY(use_device(c->device));
   std::lock_guard<std::mutex> g(c->mu);
-  const size_t nb = 16 * p->W, nc = b64_chars(nb), stride = align256(nc + 16);
-  if (p->io.ensure(5 * stride) != hipSuccess) return fail(AMPH_E_NOMEM, "party session text staging");
+  const size_t nc = b64_chars(16 * p->W);
   hipStream_t s;
   if (int st = host_stream0(c, &s)) return st;
   if (int st = party_open_post(p, is_player0, s)) return st;
-  char* d = (char*)p->io.p;
-  char* const dout[5] = {d, d + stride, d + 2 * stride, d + 3 * stride, d + 4 * stride};
-  if (int st = party_b64(p, dout, s)) return st;
-  HIP_TRY(read_back(s, {{fields_b64[0], d, nc}, {fields_b64[1], d + stride, nc}, {fields_b64[2], d + 2 * stride, nc},
-                        {fields_b64[3], d + 3 * stride, nc}, {fields_b64[4], d + 4 * stride, nc}}));
+  if (int st = party_b64(p, s)) return st;
+  char** d = p->b64;
+  HIP_TRY(read_back(s, {{fields_b64[0], d[0], nc}, {fields_b64[1], d[1], nc}, {fields_b64[2], d[2], nc},
+                        {fields_b64[3], d[3], nc}, {fields_b64[4], d[4], nc}}));
   p->finished = true;
   return AMPH_OK;
 }
@@ -2176,18 +2224,17 @@ int amph_party_partner_dev(amph_party* p, int slot, const char* text, size_t len
   return AMPH_OK;
 }
 
-int amph_party_finish_b64_dev(amph_party* p, int is_player0, char* const fields_b64[5], void* stream) {
+int amph_party_finish_b64_dev(amph_party* p, int is_player0, const char* fields_b64[5], void* stream) {
   if (int st = party_check(p)) return st;
   if (int st = party_mode(p, true)) return st;
   if (!fields_b64) return fail(AMPH_E_PARAM, "null field array");
-  for (int k = 0; k < 5; ++k)
-    if (p->W && !fields_b64[k]) return fail(AMPH_E_PARAM, "null field text");
   amph_ctx* c = p->c;
   HIP_TRY(use_device(c->device));
   std::lock_guard<std::mutex> g(c->mu);
   p->dstream = (hipStream_t)stream;
   if (int st = party_open_post(p, is_player0, p->dstream)) return st;
-  if (int st = party_b64(p, fields_b64, p->dstream)) return st;
+  if (int st = party_b64(p, p->dstream)) return st;
+  for (int k = 0; k < 5; ++k) fields_b64[k] = p->b64[k];
   p->finished = true;
   return AMPH_OK;
 }
@@ -2199,6 +2246,9 @@ void amph_party_free(amph_party* p) {
     std::lock_guard<std::mutex> g(p->c->mu);
     if (p->dev) (void)hipStreamSynchronize(p->dstream);
     else if (p->c->streams[0]) (void)hipStreamSynchronize(p->c->streams[0]);
+    // the buffers go back to the context for the next session
+    for (DevBuf* b : {&p->mem, &p->tmp, &p->io}) pool_put(p->c, *b);
+    for (DevBuf& b : p->pbuf) pool_put(p->c, b);
   }
   delete p;
 }

@@ -276,6 +276,63 @@ __global__ __launch_bounds__(kB64Block) void k_b64_words_blk(const uint4* in, ch
     dst[q] = make_uint4(lds[4 * q], lds[4 * q + 1], lds[4 * q + 2], lds[4 * q + 3]);
 }
 
+// Several equal-length byte streams (the five ODO fields of a party session)
+// in ONE launch: blockIdx.y = the stream; each workgroup codes 256 12-byte
+// units, staged through LDS as k_b64_encode_blk when they are all whole and
+// the buffers 16-byte aligned, else unit by unit as k_b64_encode (the streams'
+// final unit, '='-padded).  One launch where five k_b64_encode_blk + five
+// tail launches queued ten.
+struct B64Streams {
+  const uint8_t* in[5];
+  char* out[5];
+};
+
+__global__ __launch_bounds__(kB64Block) void k_b64_encode_multi(B64Streams st, size_t nbytes) {
+  __shared__ uint32_t lds[3 * kB64Block];
+  const uint8_t* in = st.in[blockIdx.y];
+  char* out = st.out[blockIdx.y];
+  const size_t units = (nbytes + 11) / 12, u0 = (size_t)blockIdx.x * kB64Block, t = u0 + threadIdx.x;
+  const bool whole = 12 * (u0 + kB64Block) <= nbytes && ((((uintptr_t)in | (uintptr_t)out) & 15) == 0);
+  if (whole) {
+    const uint4* src = reinterpret_cast<const uint4*>(in + 12 * u0);
+    for (int q = threadIdx.x; q < 3 * kB64Block / 4; q += kB64Block) {
+      const uint4 v = ldnt4(src + q);
+      lds[4 * q] = v.x; lds[4 * q + 1] = v.y; lds[4 * q + 2] = v.z; lds[4 * q + 3] = v.w;
+    }
+    __syncthreads();
+    uint8_t b[12];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const uint32_t x = lds[3 * threadIdx.x + q];
+      b[4 * q] = x & 0xFF; b[4 * q + 1] = (x >> 8) & 0xFF;
+      b[4 * q + 2] = (x >> 16) & 0xFF; b[4 * q + 3] = x >> 24;
+    }
+    uint32_t g[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) g[q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
+    st16(out + 16 * t, make_uint4(g[0], g[1], g[2], g[3]));
+    return;
+  }
+  if (t >= units) return;
+  const size_t base = 12 * t, rem = nbytes - base < 12 ? nbytes - base : 12;
+  uint8_t b[12];
+#pragma unroll
+  for (int q = 0; q < 12; ++q) b[q] = (size_t)q < rem ? in[base + q] : 0;
+  uint32_t g[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) g[q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
+  char* o = out + 16 * t;
+  const int groups = (int)((rem + 2) / 3);
+  for (int q = 0; q < groups; ++q) {
+    const int have = (int)rem - 3 * q;
+    for (int k = 0; k < 4; ++k) {
+      char ch = (char)((g[q] >> (8 * k)) & 0xFF);
+      if (k >= 2 && have < k) ch = '=';
+      o[4 * q + k] = ch;
+    }
+  }
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 unsigned grid_n(size_t n, const LaunchCfg& c) {
@@ -300,6 +357,21 @@ hipError_t launch_b64_encode(const uint8_t* in, size_t nbytes, char* out, const 
   if (nblk) AMPH_LAUNCH(k_b64_encode_blk, dim3((unsigned)nblk), dim3(kB64Block), c0, in, out);
   AMPH_LAUNCH(k_b64_encode, dim3(grid_n(units - done, c)), dim3(c.block), nblk ? c1 : c, in + 12 * done,
               nbytes - 12 * done, out + 16 * done);
+  return hipGetLastError();
+}
+
+hipError_t launch_b64_encode_multi(const uint8_t* const* in, char* const* out, int n, size_t nbytes,
+                                   const LaunchCfg& c) {
+  if (nbytes == 0 || n <= 0) return hipSuccess;
+  if (n > 5) return hipErrorInvalidValue;
+  B64Streams st{};
+  for (int k = 0; k < n; ++k) {
+    st.in[k] = in[k];
+    st.out[k] = out[k];
+  }
+  const size_t units = (nbytes + 11) / 12;
+  AMPH_LAUNCH(k_b64_encode_multi, dim3((unsigned)((units + kB64Block - 1) / kB64Block), (unsigned)n),
+              dim3(kB64Block), c, st, nbytes);
   return hipGetLastError();
 }
 

@@ -31,6 +31,7 @@
 #include <algorithm>
 
 #include "kernels.hpp"
+#include "decimal.hpp"
 
 namespace amph {
 
@@ -100,70 +101,6 @@ __device__ __forceinline__ int to_chunks(const uint4& m, uint32_t (&ch)[5]) {
 #pragma unroll
   for (int k = 1; k < 5; ++k) top = ch[k] ? k : top;
   return 9 * top + ndigits32(ch[top]);
-}
-
-__device__ __forceinline__ bool is_zero(const uint4& m) { return (m.x | m.y | m.z | m.w) == 0; }
-
-// 10^0 .. 10^38 as 128-bit little-endian limbs (10^38 < 2^128 < 10^39)
-__device__ const uint32_t kPow10[39][4] = {
-    {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x0000000au, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x00000064u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x000003e8u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x00002710u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x000186a0u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x000f4240u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x00989680u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x05f5e100u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x3b9aca00u, 0x00000000u, 0x00000000u, 0x00000000u},
-    {0x540be400u, 0x00000002u, 0x00000000u, 0x00000000u},
-    {0x4876e800u, 0x00000017u, 0x00000000u, 0x00000000u},
-    {0xd4a51000u, 0x000000e8u, 0x00000000u, 0x00000000u},
-    {0x4e72a000u, 0x00000918u, 0x00000000u, 0x00000000u},
-    {0x107a4000u, 0x00005af3u, 0x00000000u, 0x00000000u},
-    {0xa4c68000u, 0x00038d7eu, 0x00000000u, 0x00000000u},
-    {0x6fc10000u, 0x002386f2u, 0x00000000u, 0x00000000u},
-    {0x5d8a0000u, 0x01634578u, 0x00000000u, 0x00000000u},
-    {0xa7640000u, 0x0de0b6b3u, 0x00000000u, 0x00000000u},
-    {0x89e80000u, 0x8ac72304u, 0x00000000u, 0x00000000u},
-    {0x63100000u, 0x6bc75e2du, 0x00000005u, 0x00000000u},
-    {0xdea00000u, 0x35c9adc5u, 0x00000036u, 0x00000000u},
-    {0xb2400000u, 0x19e0c9bau, 0x0000021eu, 0x00000000u},
-    {0xf6800000u, 0x02c7e14au, 0x0000152du, 0x00000000u},
-    {0xa1000000u, 0x1bceccedu, 0x0000d3c2u, 0x00000000u},
-    {0x4a000000u, 0x16140148u, 0x00084595u, 0x00000000u},
-    {0xe4000000u, 0xdcc80cd2u, 0x0052b7d2u, 0x00000000u},
-    {0xe8000000u, 0x9fd0803cu, 0x033b2e3cu, 0x00000000u},
-    {0x10000000u, 0x3e250261u, 0x204fce5eu, 0x00000000u},
-    {0xa0000000u, 0x6d7217cau, 0x431e0faeu, 0x00000001u},
-    {0x40000000u, 0x4674edeau, 0x9f2c9cd0u, 0x0000000cu},
-    {0x80000000u, 0xc0914b26u, 0x37be2022u, 0x0000007eu},
-    {0x00000000u, 0x85acef81u, 0x2d6d415bu, 0x000004eeu},
-    {0x00000000u, 0x38c15b0au, 0xc6448d93u, 0x0000314du},
-    {0x00000000u, 0x378d8e64u, 0xbead87c0u, 0x0001ed09u},
-    {0x00000000u, 0x2b878fe8u, 0x72c74d82u, 0x00134261u},
-    {0x00000000u, 0xb34b9f10u, 0x7bc90715u, 0x00c097ceu},
-    {0x00000000u, 0x00f436a0u, 0xd5da46d9u, 0x0785ee10u},
-    {0x00000000u, 0x098a2240u, 0x5a86c47au, 0x4b3b4ca8u}};
-
-__device__ __forceinline__ bool ge128(const uint4& a, const uint32_t (&b)[4]) {
-  uint32_t br;
-  __builtin_subc(a.x, b[0], 0u, &br);
-  __builtin_subc(a.y, b[1], br, &br);
-  __builtin_subc(a.z, b[2], br, &br);
-  __builtin_subc(a.w, b[3], br, &br);
-  return br == 0;
-}
-
-// Decimal digit count of a 128-bit magnitude (1 for zero) without the
-// base-10^9 split: t = floor(bits * log10(2)) (bits * 1233 >> 12 is exact
-// for bits <= 128) is the count or one less, decided by one compare with 10^t.
-__device__ __forceinline__ int ndigits128(const uint4& m) {
-  const int bits = m.w ? 128 - __clz(m.w) : m.z ? 96 - __clz(m.z) : m.y ? 64 - __clz(m.y)
-                                                                   : 32 - __clz(m.x);
-  const int t = (bits * 1233) >> 12;
-  const int n = t + (ge128(m, kPow10[t]) ? 1 : 0);
-  return n ? n : 1;
 }
 
 
@@ -317,19 +254,42 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_single(uint64_t* x, size_t 
   if (threadIdx.x == 0) x[n] = carry;
 }
 
-// x[i] <- exclusive prefix (bsum already scanned); x[n] <- total (+ the map)
+// x[i] <- exclusive prefix; x[n] <- total (+ the map).  bsum holds the
+// per-workgroup sums (k_scan_reduce); wave 0 adds those before its own
+// workgroup (and the last workgroup all of them), so no launch scans them in
+// between (a single-workgroup scan launch cost ~5 us).
 __global__ __launch_bounds__(kScanBlock) void k_scan_apply(uint64_t* x, size_t n,
                                                        const uint64_t* bsum, size_t nb,
                                                        uint4* map, size_t nmap) {
+  __shared__ uint64_t sbase[2];
   const size_t i = (size_t)blockIdx.x * kScanBlock + threadIdx.x;
-  uint64_t total;
   const uint64_t v = i < n ? x[i] : 0;
-  const uint64_t e = block_excl_scan(v, &total);
-  if (i < n) {
-    x[i] = bsum[blockIdx.x] + e;
-    span_map(map, nmap, i, bsum[blockIdx.x] + e, v);
+  if (threadIdx.x < 64) {
+    const bool last = blockIdx.x + 1 == gridDim.x;
+    uint64_t b = 0, t = 0;
+    for (size_t k = threadIdx.x; k < nb; k += 64) {
+      const uint64_t y = bsum[k];
+      if (k < blockIdx.x) b += y;
+      if (last) t += y;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      b += __shfl_xor(b, o, 64);
+      t += __shfl_xor(t, o, 64);
+    }
+    if (threadIdx.x == 0) {
+      sbase[0] = b;
+      sbase[1] = t;
+    }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) x[n] = bsum[nb];
+  uint64_t total;
+  const uint64_t e = block_excl_scan(v, &total);  // (its barriers publish sbase)
+  const uint64_t base = sbase[0];
+  if (i < n) {
+    x[i] = base + e;
+    span_map(map, nmap, i, base + e, v);
+  }
+  if (blockIdx.x + 1 == gridDim.x && threadIdx.x == 0) x[n] = sbase[1];
 }
 
 // Encode pass 1: the text length of each workgroup's run of entries
@@ -364,10 +324,11 @@ __global__ __launch_bounds__(4 * kXBlock) void k_xenc_bsum(const uint4* mag, con
 // at the same offset mod 16 as its destination (sh), so every 16-byte unit
 // wholly inside it moves as one aligned ds_read_b128 + global 16-byte store;
 // the up to 15 bytes at either end go out singly.
+// bs[bstride * b] = the offset of workgroup b's run, bs[nblocks] the total.
 __global__ __launch_bounds__(kXBlock) void k_xenc_write(const uint4* mag, const uint8_t* neg,
                                                     size_t npairs, const uint64_t* bs,
                                                     size_t nblocks, char* out,
-                                                    unsigned long long* out_len) {
+                                                    unsigned long long* out_len, int bstride) {
   __shared__ uint4 bufv[(kXBlock * kXEntry + 8) / 16 + 2];
   char* buf = reinterpret_cast<char*>(bufv);
   const size_t k = (size_t)blockIdx.x * kXBlock + threadIdx.x;
@@ -384,7 +345,7 @@ __global__ __launch_bounds__(kXBlock) void k_xenc_write(const uint4* mag, const 
     len = 11 + nd + sd + ne + se + (k + 1 < npairs);
   }
   const uint32_t loc = block_excl_scan32(len, &total);
-  const uint64_t base = bs[blockIdx.x];
+  const uint64_t base = bs[(size_t)bstride * blockIdx.x];
   char* dst = out + 1 + base;  // out[0] = '['
   const size_t sh = (uintptr_t)dst & 15;
   if (k < npairs) {
@@ -1155,7 +1116,8 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64
 // first value index (and the map k_open_post starts from), and any kWsBit sends
 // the whole text through k_xdec_slow, which writes pair order instead.
 __global__ __launch_bounds__(kDecBlock) void k_xdec_span(Text text, uint64_t* cnt, uint4* smag,
-                                                     uint8_t* sneg) {
+                                                     uint8_t* sneg, unsigned long long* bad) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *bad = kNoFail;  // (the passes after this one report into it)
   __shared__ uint4 win4[kWin / 16 + 1];
   __shared__ uint16_t pos[kXSpanSlots];  // colon, relative to b0
   __shared__ int sfail;
@@ -1217,12 +1179,10 @@ hipError_t scan_u64(uint64_t* x, size_t n, uint64_t* bsum, LaunchCfg c, uint4* m
     AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c, x, n, map, nmap);
     return hipGetLastError();
   }
-  LaunchCfg c0 = c, c1 = c, c2 = c;
+  LaunchCfg c0 = c, c2 = c;
   c0.ev_stop = nullptr;
-  c1.ev_start = c1.ev_stop = nullptr;
   c2.ev_start = nullptr;
   AMPH_LAUNCH(k_scan_reduce, dim3(nb), dim3(kScanBlock), c0, x, n, bsum);
-  AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c1, bsum, (size_t)nb, (uint4*)nullptr, (size_t)0);
   AMPH_LAUNCH(k_scan_apply, dim3(nb), dim3(kScanBlock), c2, x, n, bsum, (size_t)nb, map, nmap);
   return hipGetLastError();
 }
@@ -1257,7 +1217,26 @@ hipError_t launch_exchange_encode(const uint4* mag, const uint8_t* neg, size_t n
     AMPH_LAUNCH(k_scan_single, dim3(1), dim3(kScanBlock), c0, bs, (size_t)0, (uint4*)nullptr, (size_t)0);
   }
   AMPH_LAUNCH(k_xenc_write, dim3(nb ? (unsigned)nb : 1u), dim3(kXBlock), c1, mag, neg, npairs, bs,
-              nb, out, out_len);
+              nb, out, out_len, 1);
+  return hipGetLastError();
+}
+
+static_assert(kXBlock == 2 * kXLenPairs, "an encode workgroup spans two K_ODO_PRE length words");
+size_t xenc_lens_scratch_bytes(size_t npairs) {
+  return 8 * ((size_t)blocks_of(blocks_of(npairs, kXLenPairs), kScanBlock) + 1);
+}
+
+// Two passes after K_ODO_PRE's lengths: their scan, then k_xenc_write
+hipError_t launch_exchange_encode_lens(const uint4* mag, const uint8_t* neg, size_t npairs, uint64_t* lens,
+                                       char* out, unsigned long long* out_len, void* scratch, const LaunchCfg& c) {
+  const size_t nl = npairs ? blocks_of(npairs, kXLenPairs) : 0, nb = npairs ? blocks_of(npairs, kXBlock) : 0;
+  LaunchCfg c0 = c, c1 = c;
+  c0.ev_stop = nullptr;
+  c1.ev_start = nullptr;
+  hipError_t e = scan_u64(lens, nl, static_cast<uint64_t*>(scratch), c0);
+  if (e != hipSuccess) return e;
+  AMPH_LAUNCH(k_xenc_write, dim3(nb ? (unsigned)nb : 1u), dim3(kXBlock), c1, mag, neg, npairs, lens, nl, out,
+              out_len, 2);
   return hipGetLastError();
 }
 
@@ -1299,8 +1278,9 @@ size_t xspan_slots(size_t len, size_t npairs) {
 size_t xspan_map_words(size_t npairs) { return blocks_of(2 * npairs, kXMapValues) + 1; }
 size_t xdec_spans_scratch_bytes(size_t len) { return 8 * ((size_t)blocks_of(xspan_spans(len), kScanBlock) + 1); }
 
-// the span pass, the scan of its count words (+ the map), the general pass
-// (+ the array check; returns at once unless a span failed or the count is off)
+// the span pass (which also resets *bad), the scan of its count words (+ the
+// map), the general pass (+ the array check and the map's windows; returns at
+// once unless a span failed or the count is off): four launches
 hipError_t launch_exchange_decode_spans(const char* text, size_t len, size_t npairs, const XSpans& out,
                                         unsigned long long* bad, void* scratch, const LaunchCfg& c) {
   const size_t mis = (uintptr_t)text & 15;
@@ -1311,7 +1291,7 @@ hipError_t launch_exchange_decode_spans(const char* text, size_t len, size_t npa
   c0.ev_stop = nullptr;
   cm.ev_start = cm.ev_stop = nullptr;
   c1.ev_start = nullptr;
-  AMPH_LAUNCH(k_xdec_span, dim3((unsigned)nb), dim3(kDecBlock), c0, t, out.base, out.mag, out.neg);
+  AMPH_LAUNCH(k_xdec_span, dim3((unsigned)nb), dim3(kDecBlock), c0, t, out.base, out.mag, out.neg, bad);
   hipError_t e = scan_u64(out.base, nb, static_cast<uint64_t*>(scratch), cm, out.map, xspan_map_words(npairs));
   if (e != hipSuccess) return e;
   AMPH_LAUNCH(k_xdec_slow<SpanBases>, dim3((unsigned)std::min<size_t>(nb, kSlowGrid)), dim3(kDecBlock), c1, t,

@@ -19,6 +19,7 @@
 #include <hip/hip_ext.h>
 
 #include "b64.hpp"
+#include "decimal.hpp"
 
 namespace amph {
 
@@ -253,12 +254,20 @@ __global__ __launch_bounds__(kPairBlock) void k_conv(const uint4* masked, const 
 // K_ODO_PRE, one Beaver pair per lane (k = 2i: (y_i, r_i), k = 2i+1: (v_i, r_i);
 // r_i = value of mask tuple 2i, v_i = value of mask tuple 2i+1), the
 // workgroup's triples (96 B) and mask tuples (32 B) staged through LDS.
-// Even lanes also write the raw y_i and r_i copies, odd lanes v_i.
+// Even lanes also write the raw y_i and r_i copies, odd lanes v_i (each
+// output optional).  (Writing the base64 text of y, r and v here instead of the
+// raw copies -- 64 instead of 48 + 112 B per word with the separate base64
+// pass -- measured 389-396 us against 290 + 3 x 30 at 4 Mi words: the
+// encoding's VALU work in every workgroup cost more than the traffic it saved.)
+// lens (the party session): the exchange text length of this workgroup's
+// 128 FactorPairs -- the exchange encoder's first pass (k_xenc_bsum), which
+// would read the diffs back, done where they are made.
+template <bool LENS>
 __global__ __launch_bounds__(kPairBlock) void k_odo_pre(const uint4* share_data, int stride_w,
                                                        const uint4* masks, const uint4* triples,
                                                        size_t pairs, uint4* oy, uint4* orr,
                                                        uint4* ov, uint4* omag, uint16_t* oneg,
-                                                       Fp f) {
+                                                       Fp f, uint64_t* lens) {
   __shared__ uint4 tri[kPairBlock * 7];
   __shared__ uint4 msk[kPairBlock * 3];
   const size_t k0 = (size_t)blockIdx.x * kPairBlock;
@@ -271,23 +280,41 @@ __global__ __launch_bounds__(kPairBlock) void k_odo_pre(const uint4* share_data,
   uint4 yr = make_uint4(0, 0, 0, 0);
   if (k < pairs && even) yr = ld(share_data + (size_t)stride_w * i);
   __syncthreads();
-  if (k >= pairs) return;
-  const unsigned lk = threadIdx.x, lpair0 = lk & ~1u;
-  const uint4 a = tri[lk * 7], b = tri[lk * 7 + 2];
-  const uint4 m1 = msk[lpair0 * 3], m2 = msk[(lpair0 + 1) * 3];
-  const uint4 x = even ? yr : m2;
-  if (even) {
-    st_party(oy + i, yr);
-    st_party(orr + i, m1);
-  } else {
-    st_party(ov + i, m2);
+  uint32_t len = 0;
+  if (k < pairs) {
+    const unsigned lk = threadIdx.x, lpair0 = lk & ~1u;
+    const uint4 a = tri[lk * 7], b = tri[lk * 7 + 2];
+    const uint4 m1 = msk[lpair0 * 3], m2 = msk[(lpair0 + 1) * 3];
+    const uint4 x = even ? yr : m2;
+    if (even) {
+      if (oy) st_party(oy + i, yr);
+      if (orr) st_party(orr + i, m1);
+    } else if (ov) {
+      st_party(ov + i, m2);
+    }
+    W4 d, e;
+    const uint32_t sd = signed_diff(redc(w4(x), f), redc(w4(a), f), d);
+    const uint32_t se = signed_diff(redc(w4(m1), f), redc(w4(b), f), e);
+    st_party(omag + 2 * k, u4(d));
+    st_party(omag + 2 * k + 1, u4(e));
+    oneg[k] = (uint16_t)(sd | (se << 8));
+    if constexpr (LENS) len = xentry_len(u4(d), sd, u4(e), se, k + 1 == pairs);
   }
-  W4 d, e;
-  const uint32_t sd = signed_diff(redc(w4(x), f), redc(w4(a), f), d);
-  const uint32_t se = signed_diff(redc(w4(m1), f), redc(w4(b), f), e);
-  st_party(omag + 2 * k, u4(d));
-  st_party(omag + 2 * k + 1, u4(e));
-  oneg[k] = (uint16_t)(sd | (se << 8));
+  if constexpr (!LENS) return;
+  // (the wave sums reuse the triples' LDS once every lane is past it: one
+  // more word of LDS would cost a workgroup per CU -- 20 KiB x 8 fills it)
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) len += __shfl_xor(len, o, 64);
+  uint32_t* wlen = reinterpret_cast<uint32_t*>(tri);
+  __syncthreads();
+  if (__lane_id() == 0) wlen[threadIdx.x >> 6] = len;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < kPairBlock / 64; ++w) t += wlen[w];
+    lens[blockIdx.x] = t;
+  }
 }
 
 // recombineDiffs: one opened value per lane (value t of 4 per source word),
@@ -937,11 +964,17 @@ hipError_t launch_convert_share(const uint4* masked, const uint4* tuples, size_t
 
 hipError_t launch_odo_pre(const uint4* share_data, int stride_w, const uint4* masks,
                           const uint4* triples, size_t words, uint4* oy, uint4* orr, uint4* ov,
-                          uint4* omag, uint32_t* oneg, const Fp& f, const LaunchCfg& c) {
+                          uint4* omag, uint32_t* oneg, const Fp& f, const LaunchCfg& c, uint64_t* lens) {
   if (words == 0) return hipSuccess;
   const size_t pairs = 2 * words;
-  AMPH_LAUNCH(k_odo_pre, dim3((unsigned)((pairs + kPairBlock - 1) / kPairBlock)), dim3(kPairBlock), c,
-              share_data, stride_w, masks, triples, pairs, oy, orr, ov, omag, (uint16_t*)oneg, f);
+  static_assert(kPairBlock == kXLenPairs, "one exchange length per K_ODO_PRE workgroup");
+  const dim3 g((unsigned)((pairs + kPairBlock - 1) / kPairBlock));
+  if (lens)
+    AMPH_LAUNCH(k_odo_pre<true>, g, dim3(kPairBlock), c, share_data, stride_w, masks, triples, pairs, oy, orr, ov,
+                omag, (uint16_t*)oneg, f, lens);
+  else
+    AMPH_LAUNCH(k_odo_pre<false>, g, dim3(kPairBlock), c, share_data, stride_w, masks, triples, pairs, oy, orr, ov,
+                omag, (uint16_t*)oneg, f, lens);
   return hipGetLastError();
 }
 

@@ -92,11 +92,14 @@ hipError_t launch_convert_share(const uint4* masked, const uint4* tuples, size_t
                                 W4 alpha_mont, int use_zero_input, uint4* out, const Fp& f,
                                 const LaunchCfg& c);
 
-// K_ODO_PRE: raw y/r/v copies + signed Beaver diffs.
+// K_ODO_PRE: raw y/r/v copies (each optional) + signed Beaver diffs; with
+// lens, also the exchange text length of every kXLenPairs FactorPairs
+// (launch_exchange_encode_lens' input).
+constexpr size_t kXLenPairs = 128;
 hipError_t launch_odo_pre(const uint4* share_data, int share_stride_words, const uint4* masks,
                           const uint4* triples, size_t words, uint4* out_y, uint4* out_r,
                           uint4* out_v, uint4* out_mag, uint32_t* out_neg, const Fp& f,
-                          const LaunchCfg& c);
+                          const LaunchCfg& c, uint64_t* lens = nullptr);
 
 // recombineDiffs: sum over parties of signed diffs mod p -> canonical opened values.
 hipError_t launch_open_diffs(const SignedSet& d, int n, size_t pairs, uint4* out_opened,
@@ -121,6 +124,9 @@ hipError_t launch_mask_words(const uint4* secrets, const uint4* masks, size_t wo
 
 // base64 wire codec (codec.hip): standard alphabet, '=' padding, no line breaks.
 hipError_t launch_b64_encode(const uint8_t* in, size_t nbytes, char* out, const LaunchCfg& c);
+// n <= 5 streams of nbytes each, one launch
+hipError_t launch_b64_encode_multi(const uint8_t* const* in, char* const* out, int n, size_t nbytes,
+                                   const LaunchCfg& c);
 // text_end: the range ends the text, so '=' may pad its last two chars
 hipError_t launch_b64_decode(const char* in, size_t nchars, uint8_t* out, size_t out_bytes,
                              unsigned long long* bad, const LaunchCfg& c, bool text_end = true);
@@ -134,11 +140,17 @@ size_t xenc_scratch_bytes(size_t npairs);
 size_t xenc_max_bytes(size_t npairs);
 hipError_t launch_exchange_encode(const uint4* mag, const uint8_t* neg, size_t npairs, char* out,
                                   unsigned long long* out_len, void* scratch, const LaunchCfg& c);
+// the same text when K_ODO_PRE has written the lengths of every kXLenPairs
+// pairs (lens: ceil(npairs / kXLenPairs) + 1 words, scanned in place)
+size_t xenc_lens_scratch_bytes(size_t npairs);
+hipError_t launch_exchange_encode_lens(const uint4* mag, const uint8_t* neg, size_t npairs, uint64_t* lens,
+                                       char* out, unsigned long long* out_len, void* scratch, const LaunchCfg& c);
 size_t xdec_scratch_bytes(size_t len);
 hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, uint4* mag,
                                   uint8_t* neg, unsigned long long* bad, void* scratch,
                                   const LaunchCfg& c);
-// decode into span form (see XSpans): one read of the text, no count pass
+// decode into span form (see XSpans): one read of the text, no count pass;
+// resets *bad itself (kNoFail) before reporting into it
 size_t xspan_spans(size_t len);
 size_t xspan_slots(size_t len, size_t npairs);  // >= both the span slots and 2 npairs
 size_t xspan_map_words(size_t npairs);

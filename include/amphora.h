@@ -377,10 +377,10 @@ int amph_exchange_decode(amph_ctx* ctx, const char* text, size_t len, size_t npa
  * 8 KiB of text in their own slots, found by finish through the decoded span
  * bases; no count pass), where amph_exchange_decode reads its text twice to
  * write pair order.  A session belongs to one context (calls are serialised by
- * its mutex), holds 524 bytes per word of device memory (the triples, five
- * fields, its own diffs and text at most) plus about 1.07 x each partner
- * text's length (that partner's diffs) and one partner text at a time until
- * amph_party_free, and may be finished once.
+ * its mutex), holds about 630 bytes per word of device memory (the triples,
+ * the five fields raw and as base64, its own diffs and text at most) plus
+ * about 1.1 x each partner text's length (that partner's diffs) and one
+ * partner text at a time until amph_party_free, and may be finished once.
  * amph_party_words = the session's word count; free sessions before their
  * context.  Status semantics
  * as the calls it replaces (amph_exchange_decode's AMPH_E_PARAM / AMPH_E_LEN
@@ -412,17 +412,18 @@ void amph_party_free(amph_party* party);
  * amph_exchange_max_chars(2 * words).  partner_dev: text is device memory of
  * the given length; *bad_index is a device word set as amph_exchange_decode's
  * device mode sets it (AMPH_NO_FAILURE when the text held) -- check it before
- * finishing.  finish_b64_dev: the five fields as base64 into device buffers
- * (amph_party_finish_b64's lengths).  A device-mode session takes only these
- * calls (and amph_party_words / amph_party_free); a multi-device context is
- * refused. */
+ * finishing.  finish_b64_dev: the five fields as base64 text in the session's
+ * device memory, *fields_b64[k] their addresses (amph_party_finish_b64's
+ * lengths; valid until amph_party_free) -- the response is sent from there.
+ * A device-mode session takes only these calls (and amph_party_words /
+ * amph_party_free); a multi-device context is refused. */
 int amph_party_begin_dev(amph_ctx* ctx, const uint8_t* share_data, size_t share_stride,
                          const uint8_t* mask_tuples, const uint8_t* triples, size_t words, int n_parties,
                          uint8_t* out_y, uint8_t* out_r, uint8_t* out_v, void* stream, amph_party** out);
 int amph_party_text_dev(amph_party* party, const char** text, const uint64_t** text_len);
 int amph_party_partner_dev(amph_party* party, int slot, const char* text, size_t len, int64_t* bad_index,
                            void* stream);
-int amph_party_finish_b64_dev(amph_party* party, int is_player0, char* const fields_b64[5], void* stream);
+int amph_party_finish_b64_dev(amph_party* party, int is_player0, const char* fields_b64[5], void* stream);
 
 /* ---- benchmark / test input generation (device pointers only) ---------- */
 /* Honest n-party ODOs: out_fields[k * n_parties + j] = field k (y,r,v,w,u) of
