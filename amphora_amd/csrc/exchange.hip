@@ -628,19 +628,20 @@ __device__ __forceinline__ bool fast_parse(const uint32_t* l32, uint32_t o, bool
   if (!after_ok(r.dend)) return false;
   const uint32_t full = nd >> 3, rem = nd & 7u;
   bool ovf = false;
+  uint32_t v[4];  // (a local, not r.v: in a persistent-loop variant r.v was kept in scratch)
   if (full == 4) {  // 32..39 digits (a random 128-bit value): two 16-digit halves
     const uint64_t p0 = (uint64_t)digits8(d[0], d[1]) * 100000000u + digits8(d[2], d[3]);
     const uint64_t p1 = (uint64_t)digits8(d[4], d[5]) * 100000000u + digits8(d[6], d[7]);
     const unsigned __int128 t = (unsigned __int128)p0 * 10000000000000000ull + p1;  // < 10^32
-    r.v[0] = (uint32_t)t;
-    r.v[1] = (uint32_t)(t >> 32);
-    r.v[2] = (uint32_t)(t >> 64);
-    r.v[3] = (uint32_t)(t >> 96);
+    v[0] = (uint32_t)t;
+    v[1] = (uint32_t)(t >> 32);
+    v[2] = (uint32_t)(t >> 64);
+    v[3] = (uint32_t)(t >> 96);
   } else {
-    r.v[0] = r.v[1] = r.v[2] = r.v[3] = 0;
+    v[0] = v[1] = v[2] = v[3] = 0;
 #pragma unroll
     for (uint32_t m = 0; m < 4; ++m)
-      if (m < full) fold(r.v, 100000000u, digits8(d[2 * m], d[2 * m + 1]), ovf);
+      if (m < full) fold(v, 100000000u, digits8(d[2 * m], d[2 * m + 1]), ovf);
   }
   if (rem) {
     uint32_t lo = d[0], hi = d[1];
@@ -650,8 +651,12 @@ __device__ __forceinline__ bool fast_parse(const uint32_t* l32, uint32_t o, bool
     const uint64_t x = ((uint64_t)hi << 32) | lo;
     const uint32_t sh = 8 * (8 - rem);  // 8..56
     const uint64_t y = (x << sh) | (0x3030303030303030ull >> (64 - sh));
-    fold(r.v, pow10_small(rem), digits8((uint32_t)y, (uint32_t)(y >> 32)), ovf);
+    fold(v, pow10_small(rem), digits8((uint32_t)y, (uint32_t)(y >> 32)), ovf);
   }
+  r.v[0] = v[0];
+  r.v[1] = v[1];
+  r.v[2] = v[2];
+  r.v[3] = v[3];
   return !ovf;
 }
 
@@ -1106,7 +1111,9 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64
 
 // The decode into span form (launch_exchange_decode_spans; the party
 // session's partner texts), ONE read of the text with no count pass before
-// it: staging and colon listing as k_xdec_fast, then each value checked
+// it (one workgroup per span: a persistent double-buffered variant whose next
+// window came in by LDS-DMA during the parse measured 294 vs 257 us,
+// profiles/r03s2_xspan_dma_ab.txt): staging and colon listing as k_xdec_fast, then each value checked
 // against its compact-layout segment without its global index (fast_value)
 // and stored at slot kXSpanSlots * span + its rank among the span's colons,
 // its byte = sign (bit 0) | key "b" (bit 1).  cnt[span] = the span's colon
