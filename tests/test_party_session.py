@@ -258,3 +258,44 @@ def test_session_device_mode_errors(ctx, F):
     assert b"host-mode party session takes the host calls" in A._lib.lib.amph_last_error()
     s.close()
     h.close()
+
+
+def test_text_length_edges(ctx, F):
+    """A partner text whose length ends a few bytes short of an 8 KiB span
+    boundary (trailing whitespace pads it: len % 8192 = 8180), decoded in host
+    mode, in device mode at an odd device address (the span count then covers
+    one span past the text), and by the pair-order decode (amph_exchange_decode,
+    host and device): the same diffs / w, u as the compact text."""
+    import torch
+    n, W = 2, 3000
+    shares, masks, triples = party_inputs(F, n, W)
+    pre = [F.odo_pre(shares[j], 32, masks[j], triples[j]) for j in range(n)]
+    t1 = ctx.party_begin(shares[1], 32, masks[1], triples[1], n).text()
+    tp = t1 + b" " * ((8180 - len(t1) % 8192) % 8192)
+    assert len(tp) % 8192 == 8180
+    opened = F.recombine_diffs([p[3] for p in pre], [p[4] for p in pre])
+    ow, ou = F.odo_post(opened, triples[0], True)
+    for text in (t1, tp):
+        s = ctx.party_begin(shares[0], 32, masks[0], triples[0], n, want_yrv=False)
+        s.partner(1, text)
+        w, u = s.finish(True)
+        assert np.array_equal(w, ow) and np.array_equal(u, ou)
+        s.close()
+        m, g = ctx.exchange_decode(text, 2 * W)
+        assert ctx.exchange_encode(m, g) == t1
+        for off in (0, 5):
+            buf = torch.zeros(len(text) + off, dtype=torch.uint8, device="cuda")
+            buf[off:] = torch.from_numpy(np.frombuffer(text, np.uint8).copy()).cuda()
+            dm, dg, bad = ctx.exchange_decode(buf[off:], 2 * W)
+            torch.cuda.synchronize()
+            assert int(bad.item()) == 0x7F7F7F7F7F7F7F7F
+            assert ctx.exchange_encode(dm.cpu().numpy(), dg.cpu().numpy()) == t1
+            dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+            sd = ctx.party_begin_dev(dev(shares[0]), 32, dev(masks[0]), dev(triples[0]), n)
+            b = sd.partner(1, buf[off:])
+            fields = sd.finish_b64(True)
+            torch.cuda.synchronize()
+            assert int(b.item()) == 0x7F7F7F7F7F7F7F7F
+            assert fields[3].cpu().numpy().tobytes() == base64.b64encode(ow.tobytes())
+            assert fields[4].cpu().numpy().tobytes() == base64.b64encode(ou.tobytes())
+            sd.close()
