@@ -381,6 +381,9 @@ int amph_exchange_decode(amph_ctx* ctx, const char* text, size_t len, size_t npa
  * the five fields raw and as base64, its own diffs and text at most) plus
  * about 1.1 x each partner text's length (that partner's diffs) and one
  * partner text at a time until amph_party_free, and may be finished once.
+ * amph_party_free hands the session's device buffers back to its context,
+ * which keeps up to 16 of them for the next session (one session per request
+ * then allocates nothing) and frees them in amph_ctx_destroy.
  * amph_party_words = the session's word count; free sessions before their
  * context.  Status semantics
  * as the calls it replaces (amph_exchange_decode's AMPH_E_PARAM / AMPH_E_LEN
