@@ -247,7 +247,7 @@ def test_session_device_mode_errors(ctx, F):
     t1 = ctx.party_begin(shares[1], 32, masks[1], triples[1], n).text()
     at = t1.index(b":") + 3
     bad_text = t1[:at] + b"x" + t1[at + 1:]
-    bad = s.partner(1, dev(np.frombuffer(bad_text, np.uint8)))
+    bad = s.partner(1, dev(np.frombuffer(bad_text, np.uint8).copy()))
     assert 6 <= int(bad.item()) <= at
     with pytest.raises(A.AmphoraNativeError, match="takes the \\*_dev calls"):
         A._lib.PartySession.finish(s, True)
@@ -299,3 +299,54 @@ def test_text_length_edges(ctx, F):
             assert fields[3].cpu().numpy().tobytes() == base64.b64encode(ow.tobytes())
             assert fields[4].cpu().numpy().tobytes() == base64.b64encode(ou.tobytes())
             sd.close()
+
+
+def test_session_partner_fuzz_matches_pair_decode(ctx, F):
+    """Mutated partner texts (a byte replaced, deleted or inserted, whitespace
+    added): the session's one-read span-form decode accepts exactly the texts
+    the pair-order decode (amph_exchange_decode: count pass + compact pass +
+    general pass) accepts, reports the same error at the same offset, and on
+    an accepted text finishes with the w, u the oracle computes from that
+    decode's diffs."""
+    rng = np.random.default_rng(7)
+    n, W = 2, 1500
+    shares, masks, triples = party_inputs(F, n, W)
+    pre0 = F.odo_pre(shares[0], 32, masks[0], triples[0])
+    t1 = ctx.party_begin(shares[1], 32, masks[1], triples[1], n).text()
+    alphabet = list(b'0123456789-,:{}[]"ab \n')
+    accepted = rejected = 0
+    for trial in range(80):
+        t = bytearray(t1)
+        pos = int(rng.integers(0, len(t)))
+        kind = trial % 4
+        if kind == 0:
+            t[pos] = int(rng.choice(alphabet))
+        elif kind == 1:
+            del t[pos]
+        elif kind == 2:
+            t.insert(pos, int(rng.choice(list(b' 0-,'))))
+        else:
+            t[pos:pos] = b" \t"
+        t = bytes(t)
+        try:
+            m, g = ctx.exchange_decode(t, 2 * W)
+            ref = None
+        except ValueError as e:
+            ref = str(e)
+        s = ctx.party_begin(shares[0], 32, masks[0], triples[0], n, want_yrv=False)
+        try:
+            s.partner(1, t)
+            got = None
+        except ValueError as e:
+            got = str(e)
+        assert got == ref, (trial, kind, pos)
+        if ref is None:
+            accepted += 1
+            w, u = s.finish(True)
+            opened = F.recombine_diffs([pre0[3], m], [pre0[4], g])
+            ow, ou = F.odo_post(opened, triples[0], True)
+            assert np.array_equal(w, ow) and np.array_equal(u, ou), (trial, kind, pos)
+        else:
+            rejected += 1
+        s.close()
+    assert accepted > 5 and rejected > 5
