@@ -211,6 +211,20 @@ __device__ __forceinline__ uint32_t signed_diff(const W4& x, const W4& a, W4& ma
 // pattern of the per-lane reads), then each lane reads its own tuple's fields.
 template <int S, int BS>
 __device__ __forceinline__ void stage_tuples(uint4* lds, const uint4* src, size_t ntuples) {
+  if (ntuples == (size_t)BS) {
+    // a whole workgroup's run: all S loads in flight before the first LDS
+    // write (the guarded loop below made the compiler wait for each load
+    // before issuing the next -- S dependent HBM latencies per workgroup)
+    uint4 v[S];
+#pragma unroll
+    for (int r = 0; r < S; ++r) v[r] = ld(src + (size_t)r * BS + threadIdx.x);
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+      const int q = r * BS + threadIdx.x;
+      lds[(q / S) * (S + 1) + q % S] = v[r];
+    }
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < S; ++r) {
     const size_t q = (size_t)r * BS + threadIdx.x;
@@ -438,7 +452,11 @@ __device__ __forceinline__ void span_pair(const uint4* mag, const uint8_t* negb,
   sg = swap ? ((ny & 1u) | ((nx & 1u) << 8)) : ((nx & 1u) | ((ny & 1u) << 8));
 }
 
-template <int NP, bool BIG, bool STAGE_MAG>
+// SPAN: parties 1 .. NP-1 are partners in the span form, party 0 this party's
+// pair-ordered diffs (the party session) -- known at compile time, so the
+// partners' window loads are issued together instead of one kernel-argument
+// test and wait per party.
+template <int NP, bool BIG, bool STAGE_MAG, bool SPAN>
 __global__ __launch_bounds__(kPairBlock) void k_open_post(SignedSet d, int n, const uint4* triples,
                                                          size_t pairs, int p0, uint4* ow, uint4* ou,
                                                          Fp f) {
@@ -452,7 +470,7 @@ __global__ __launch_bounds__(kPairBlock) void k_open_post(SignedSet d, int n, co
   if constexpr (NP > 0) {
 #pragma unroll
     for (int j = 0; j < NP; ++j)
-      if (!STAGE_MAG && d.sbase[j]) span_win(d.sbase[j], d.smap[j], d.snb[j], pairs, sw[j]);
+      if (SPAN && j > 0) span_win(d.sbase[j], d.smap[j], d.snb[j], pairs, sw[j]);
   }
   stage_tuples<6, kPairBlock>(tri, triples + 6 * k0, nblk);
   W4 D = {}, E = {};
@@ -466,7 +484,7 @@ __global__ __launch_bounds__(kPairBlock) void k_open_post(SignedSet d, int n, co
     }
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      if (!STAGE_MAG && d.sbase[j]) {  // a partner's decoded text in span form
+      if (SPAN && j > 0) {  // a partner's decoded text in span form
         md[j] = me[j] = make_uint4(0, 0, 0, 0);
         sg[j] = 0;
         if (k < pairs)
@@ -1008,11 +1026,17 @@ hipError_t launch_open_post(const SignedSet& d, int n, const uint4* triples, siz
   if (words == 0) return hipSuccess;
   const size_t pairs = 2 * words;
   const dim3 g((unsigned)((pairs + kPairBlock - 1) / kPairBlock));
-#define L(NP, BIG)                                                                                  \
-  if (stage_mag) AMPH_LAUNCH((k_open_post<NP, BIG, true>), g, dim3(kPairBlock), c, d, n, triples,  \
-                             pairs, p0, ow, ou, f);                                                \
-  else AMPH_LAUNCH((k_open_post<NP, BIG, false>), g, dim3(kPairBlock), c, d, n, triples, pairs, p0, \
-                   ow, ou, f)
+  // span-form partners: all of parties 1 .. n-1 (the session), never party 0
+  const bool span = n > 1 && d.sbase[1];
+  for (int j = 0; j < n; ++j)
+    if ((d.sbase[j] != nullptr) != (span && j > 0)) return hipErrorInvalidValue;
+#define L(NP, BIG)                                                                                        \
+  if (stage_mag) AMPH_LAUNCH((k_open_post<NP, BIG, true, false>), g, dim3(kPairBlock), c, d, n, triples, \
+                             pairs, p0, ow, ou, f);                                                      \
+  else if (span) AMPH_LAUNCH((k_open_post<NP, BIG, false, true>), g, dim3(kPairBlock), c, d, n, triples, \
+                             pairs, p0, ow, ou, f);                                                      \
+  else AMPH_LAUNCH((k_open_post<NP, BIG, false, false>), g, dim3(kPairBlock), c, d, n, triples, pairs,  \
+                   p0, ow, ou, f)
   if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
 #undef L
   return hipGetLastError();
