@@ -419,7 +419,8 @@ void amph_party_free(amph_party* party);
  * device memory, *fields_b64[k] their addresses (amph_party_finish_b64's
  * lengths; valid until amph_party_free) -- the response is sent from there.
  * A device-mode session takes only these calls (and amph_party_words /
- * amph_party_free); a multi-device context is refused. */
+ * amph_party_free; amph_party_text_len reads 0 for it -- its length is the
+ * device word); a multi-device context is refused. */
 int amph_party_begin_dev(amph_ctx* ctx, const uint8_t* share_data, size_t share_stride,
                          const uint8_t* mask_tuples, const uint8_t* triples, size_t words, int n_parties,
                          uint8_t* out_y, uint8_t* out_r, uint8_t* out_v, void* stream, amph_party** out);
