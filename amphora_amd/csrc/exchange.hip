@@ -338,10 +338,12 @@ __global__ __launch_bounds__(kXBlock) void k_xenc_write(const uint4* mag, const 
   uint32_t len = 0, total;  // <= 92 per entry, <= 23 552 per workgroup
   if (k < npairs) {
     const uint4 d = mag[2 * k], e = mag[2 * k + 1];
+    const uint32_t ng = reinterpret_cast<const uint16_t*>(neg)[k];  // (loaded beside the magnitudes)
+    __builtin_amdgcn_sched_barrier(0);
     nd = to_chunks(d, cd);
     ne = to_chunks(e, ce);
-    sd = neg[2 * k] != 0 && !is_zero(d);  // BigInteger has no negative zero
-    se = neg[2 * k + 1] != 0 && !is_zero(e);
+    sd = (ng & 0xFFu) != 0 && !is_zero(d);  // BigInteger has no negative zero
+    se = (ng >> 8) != 0 && !is_zero(e);
     len = 11 + nd + sd + ne + se + (k + 1 < npairs);
   }
   const uint32_t loc = block_excl_scan32(len, &total);
@@ -1073,6 +1075,7 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64
     const int c2 = min((int)threadIdx.x + 2 * kDecBlock, kWin / 16);
     const u32x4 v0 = __builtin_nontemporal_load(a + threadIdx.x),
                 v1 = __builtin_nontemporal_load(a + threadIdx.x + kDecBlock), v2 = __builtin_nontemporal_load(a + c2);
+    __builtin_amdgcn_sched_barrier(0);  // (all three in flight first, as in k_xdec_span)
     win4[threadIdx.x] = make_uint4(v0.x, v0.y, v0.z, v0.w);
     win4[threadIdx.x + kDecBlock] = make_uint4(v1.x, v1.y, v1.z, v1.w);
     if ((int)threadIdx.x + 2 * kDecBlock <= kWin / 16) win4[c2] = make_uint4(v2.x, v2.y, v2.z, v2.w);
@@ -1137,6 +1140,9 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_span(Text text, uint64_t* cn
     const int c2 = min((int)threadIdx.x + 2 * kDecBlock, kWin / 16);
     const u32x4 v0 = __builtin_nontemporal_load(a + threadIdx.x),
                 v1 = __builtin_nontemporal_load(a + threadIdx.x + kDecBlock), v2 = __builtin_nontemporal_load(a + c2);
+    // all three loads in flight before the first LDS write (the scheduler
+    // otherwise sank the third below the first two writes' waits)
+    __builtin_amdgcn_sched_barrier(0);
     win4[threadIdx.x] = make_uint4(v0.x, v0.y, v0.z, v0.w);
     win4[threadIdx.x + kDecBlock] = make_uint4(v1.x, v1.y, v1.z, v1.w);
     if ((int)threadIdx.x + 2 * kDecBlock <= kWin / 16) win4[c2] = make_uint4(v2.x, v2.y, v2.z, v2.w);
