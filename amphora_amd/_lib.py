@@ -634,11 +634,15 @@ class Context:
 
     # -- synthetic device inputs (bench / tests) --------------------------------
     def synth_odos(self, seed: int, n: int, words: int, fault_index: int = -1,
-                   noncanon_permille: int = 0, with_plain: bool = False):
+                   noncanon_permille: int = 0, with_plain: bool = False, buf=None):
         """Returns (odos, buffer, plain_y): a (5, n, W, 16) uint8 device
-        tensor, the per-party (y, r, v, w, u) views of it, optional secrets."""
+        tensor, the per-party (y, r, v, w, u) views of it, optional secrets.
+        `buf`: generate into the caller's (5, n, W, 16) device tensor."""
         import torch
-        buf = torch.empty((5, n, words, 16), dtype=torch.uint8, device="cuda:%d" % self.device)
+        if buf is None:
+            buf = torch.empty((5, n, words, 16), dtype=torch.uint8, device="cuda:%d" % self.device)
+        elif tuple(buf.shape) != (5, n, words, 16) or buf.dtype != torch.uint8 or not buf.is_contiguous():
+            raise ValueError("buf must be a contiguous (5, n, words, 16) uint8 device tensor")
         plain = torch.empty((words, 16), dtype=torch.uint8, device=buf.device) if with_plain else None
         ptrs = (C.c_void_p * (5 * n))(*[buf[k, j].data_ptr() for k in range(5) for j in range(n)])
         stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -647,9 +651,12 @@ class Context:
         odos = [tuple(buf[k, j] for k in range(5)) for j in range(n)]
         return odos, buf, plain
 
-    def synth_words(self, seed: int, count: int):
+    def synth_words(self, seed: int, count: int, out=None):
         import torch
-        out = torch.empty((count, 16), dtype=torch.uint8, device="cuda:%d" % self.device)
+        if out is None:
+            out = torch.empty((count, 16), dtype=torch.uint8, device="cuda:%d" % self.device)
+        elif tuple(out.shape) != (count, 16) or out.dtype != torch.uint8 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous (count, 16) uint8 device tensor")
         stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         self._check(lib.amph_synth_words(self._h, seed, count, _ptr(out), stream))
         return out

@@ -1,28 +1,33 @@
 """Benchmark: device-resident share-encode + recombine+verify, secret words/s.
 
-One step = one pass of the hot path over one batch of W words per GPU:
+One step = one pass of the hot path over one batch of words:
   K_MASK  createSecret arithmetic: verify the N-party Input Mask ODOs and mask
           every secret word (DefaultAmphoraClient.java:150-160)
   K_RV    getSecret arithmetic: recombine the N-party share ODOs and verify
           the MACs (DefaultAmphoraClient.java:206-217,476-505)
 Inputs are synthetic honest N-party ODOs generated on the device (seeded),
-resident in HBM before the timed region.  Default workload = BASELINE config
-C2: 2^20 words per GPU, 2 parties, the reference's test prime.
+resident in HBM before the timed region.
+
+Default workload at EVERY world size = BASELINE config C4: 2^26 words in
+total, 2 parties, the reference's test prime, one contiguous 2^26 / N-word
+shard resident on each rank (strong scaling, no data-path collective), so
+the N = 1, 2, 4, 8 lines are points of one curve.  The per-step verify
+verdicts are combined with one RCCL all-reduce(MIN) of the per-step
+first-fail vector after the last step.  `--workload c2|c3` runs the per-GPU
+(weak-scaling) C2 / C3 arrays instead (builder-side lines).
 
 Multi-GPU (one rank per GPU): `--gpus N` under torch.distributed.run, or
 `--gpus N` alone, which starts torch.distributed.run itself as a child
-process before anything touches the GPU.  At N > 1 the default workload is
-BASELINE config C4: 2^26 words in total, 2 parties, one contiguous
-2^26 / N-word shard resident on each rank (strong scaling, no data-path
-collective); the per-step verify verdicts are combined with one RCCL
-all-reduce(MIN) of the per-step first-fail vector after the last step.
-`--workload c4` runs the same 2^26-word job at N = 1.
+process before anything touches the GPU.  With a process group the line
+also carries `scatter_gather`: the same C4 job with the whole arrays held by
+rank 0, scattered and gathered every step by one grouped RCCL send/recv
+batch per direction over xGMI (SURVEY.md 8e's second curve).
 
 Prints ONE JSON line (rank 0).  Per-kernel HIP-event timings on the launch
 stream (--samples launches of each kernel, spread over the timed steps) feed
-`roofline`; `cpu_baseline` times the C oracle (a multithreaded
-port of the reference's BigInteger algorithm) on a bounded sample, rank 0 at
-N=1 only.
+`roofline`; `cpu_baseline` times the C oracle (a multithreaded port of the
+reference's BigInteger algorithm) on a bounded sample, on rank 0 at every
+world size, after all GPU work and the process group are done.
 """
 from __future__ import annotations
 
@@ -124,11 +129,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--workload", choices=["auto", "c2", "c3", "c4"], default="auto",
-                    help="device mode: BASELINE config; auto = C2 (2^20 words per GPU) at one "
-                         "rank, C4 (2^26 words split over the ranks) at several")
+                    help="device mode: BASELINE config; auto = C4 (2^26 words in total, 2 parties, "
+                         "split over the ranks) at every world size; c2 / c3 are per-GPU "
+                         "(weak-scaling) builder-side lines")
     ap.add_argument("--words", type=int, default=None,
-                    help="words per GPU (custom device workload; host mode: words per rank; "
-                         "--scatter: total words)")
+                    help="words per GPU (custom device workload; host mode: words per rank)")
     ap.add_argument("--parties", type=int, default=None)
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher rehearsal without a GPU: rendezvous, shard ranges, the "
@@ -156,24 +161,25 @@ def parse():
                     help="rehearsal: every rank uses cuda:0 (only with --backend gloo)")
     ap.add_argument("--dist", action="store_true",
                     help="create the process group even at world size 1 (runs the RCCL "
-                         "verdict reduction / scatter path on one GPU)")
-    ap.add_argument("--scatter", action="store_true",
-                    help="C4: --words is the TOTAL array, held on rank 0 and scattered / "
-                         "gathered over RCCL every step (strong scaling)")
+                         "verdict reduction / scatter-gather path on one GPU)")
+    ap.add_argument("--no-scatter-gather", action="store_true",
+                    help="skip the root-held (RCCL scatter/gather-inclusive) C4 measurement that "
+                         "follows the device-resident one when a process group exists")
+    ap.add_argument("--sg-steps", type=int, default=3)
+    ap.add_argument("--sg-warmup", type=int, default=1)
     a = ap.parse_args()
-    world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
     if a.workload == "auto":
-        a.workload = "c2" if world == 1 else "c4"
+        a.workload = "c4"
     wl_words, wl_parties, a.scaling = WORKLOADS[a.workload]
     if a.words is None:
-        a.words = (1 << 20) if (a.mode == "host" or a.scatter) else wl_words
+        a.words = (1 << 20) if a.mode == "host" else wl_words
     else:
         a.workload, a.scaling = "custom", "weak"
     if a.parties is None:
-        a.parties = 2 if (a.mode == "host" or a.scatter or a.workload == "custom") else wl_parties
+        a.parties = 2 if (a.mode == "host" or a.workload == "custom") else wl_parties
     elif a.parties != wl_parties and a.workload != "custom":
         a.workload, a.scaling = "custom", "weak"
-    bulk = a.mode == "host" or a.scatter
+    bulk = a.mode == "host"
     if a.steps is None:
         a.steps = 5 if bulk else 1000
     if a.warmup is None:
@@ -181,86 +187,94 @@ def parse():
     return a
 
 
-def scatter_mode(a, A, torch, dist, ctx, rank, world):
-    """BASELINE C4: the full W-word arrays live on rank 0's GPU; each step
-    scatters the 10N+1 input arrays in contiguous shards over RCCL (xGMI),
-    runs K_MASK + K_RV on every shard, and gathers the masked words and the
-    canonical secrets back to rank 0; the verdict is min-combined.  Reported
-    in DESIGN.md next to the device-resident curve (not the headline)."""
-    from amphora_amd.shard import shard_range, scatter_words, gather_words, NO_FAILURE
-    W, n = a.words, a.parties
-    coll = dist.is_initialized()  # world > 1, or --dist at world 1
-    like = torch.empty((0, 16), dtype=torch.uint8, device="cuda")
-    full_in = None
-    if rank == 0:
-        _, mb, _ = ctx.synth_odos(seed=21, n=n, words=W)
-        _, sb, splain = ctx.synth_odos(seed=22, n=n, words=W, with_plain=True)
-        sec = ctx.synth_words(seed=23, count=W)
-        full_in = [mb[k, j] for k in range(5) for j in range(n)] + \
-                  [sb[k, j] for k in range(5) for j in range(n)] + [sec]
-    start, count = shard_range(W, rank, world)
-    ff = torch.full((2,), NO_FAIL, dtype=torch.int64, device="cuda")
-    flags = A._lib.AMPH_F_DEVICE | A._lib.AMPH_F_ACCUMULATE
+def scatter_gather_phase(a, A, torch, dist, ctx, rank, world, value_resident):
+    """BASELINE C4 with the arrays held by ONE GPU, after the
+    device-resident measurement: rank 0 holds the 10N+1 whole W-word input
+    arrays (N-party mask ODOs, N-party share ODOs, secrets) and every step
+    scatters them in contiguous shards, runs K_MASK + K_RV on each shard and
+    gathers the masked words and canonical secrets straight into rank 0's
+    output array.  Each direction is ONE grouped point-to-point batch
+    (`RootScatterGather`: RCCL ncclGroupStart / ncclSend x peers x arrays /
+    ncclRecv / ncclGroupEnd over xGMI); nothing is allocated per step.
+    Returns the `scatter_gather` sub-object of rank 0's line."""
     import ctypes as C
+    from amphora_amd.shard import RootScatterGather
+    lib = A._lib
+    W, n = a.words, a.parties
+    sg = RootScatterGather(W, 10 * n + 1, 2, device="cuda")
+    full_in = full_out = splain = None
+    if rank == 0:
+        full_in = torch.empty((10 * n + 1, W, 16), dtype=torch.uint8, device="cuda")
+        ctx.synth_odos(seed=21, n=n, words=W, buf=full_in[:5 * n].view(5, n, W, 16))
+        _, _, splain = ctx.synth_odos(seed=22, n=n, words=W, with_plain=True,
+                                      buf=full_in[5 * n:10 * n].view(5, n, W, 16))
+        ctx.synth_words(seed=23, count=W, out=full_in[10 * n])
+        full_out = torch.empty((2, W, 16), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    count = sg.count
+    ff = torch.full((2,), NO_FAIL, dtype=torch.int64, device="cuda")
     ffp = [C.cast(C.c_void_p(ff.data_ptr() + 8 * i), C.POINTER(C.c_int64)) for i in range(2)]
-
-    last = {}
+    flags = lib.AMPH_F_DEVICE | lib.AMPH_F_ACCUMULATE
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    structs = {}
 
     def step():
-        if coll:
-            parts = [scatter_words(full_in[i] if rank == 0 else None, W, 16, like=like)
-                     for i in range(10 * n + 1)]
-        else:
-            parts = full_in
-        mo = [tuple(parts[k * n + j] for k in range(5)) for j in range(n)]
-        so = [tuple(parts[5 * n + k * n + j] for k in range(5)) for j in range(n)]
-        marr, _ = ctx._odo_structs(mo)
-        sarr, _ = ctx._odo_structs(so)
-        masked = torch.empty((count, 16), dtype=torch.uint8, device="cuda")
-        ys = torch.empty((count, 16), dtype=torch.uint8, device="cuda")
-        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-        assert A._lib.lib.amph_mask_input(ctx._h, marr, n, parts[10 * n].data_ptr(), count,
-                                          masked.data_ptr(), ffp[0], flags, stream) == 0
-        assert A._lib.lib.amph_recombine_verify(ctx._h, sarr, n, ys.data_ptr(), ffp[1], flags,
-                                                stream) == 0
-        if coll:
-            gather_words(masked, W, 16)
-            last["ys"] = gather_words(ys, W, 16)
-            v = ff.min().view(1).clone()
-            dist.all_reduce(v, op=dist.ReduceOp.MIN)
-        else:
-            last["ys"] = ys
+        local = sg.scatter(full_in)
+        out = sg.out_view(full_out)
+        if count:
+            if not structs:  # the shard views never move: build the ODO structs once
+                structs["m"] = ctx._odo_structs([tuple(local[k * n + j] for k in range(5)) for j in range(n)])
+                structs["s"] = ctx._odo_structs([tuple(local[5 * n + k * n + j] for k in range(5))
+                                                 for j in range(n)])
+            assert lib.lib.amph_mask_input(ctx._h, structs["m"][0], n, local[10 * n].data_ptr(), count,
+                                           out[0].data_ptr(), ffp[0], flags, stream) == 0
+            assert lib.lib.amph_recombine_verify(ctx._h, structs["s"][0], n, out[1].data_ptr(), ffp[1],
+                                                 flags, stream) == 0
+        sg.gather(full_out)
 
-    for _ in range(a.warmup):
+    for _ in range(a.sg_warmup):
         step()
     torch.cuda.synchronize()
-    if coll:
-        dist.barrier()
+    dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for _ in range(a.sg_steps):
         step()
     torch.cuda.synchronize()
-    if coll:
-        dist.barrier()
+    dist.barrier()
     el = time.perf_counter() - t0
-    if coll:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = t.item()
-        fl = ff.min().view(1).clone()
-        dist.all_reduce(fl, op=dist.ReduceOp.MIN)
-        ok = int(fl.item()) == NO_FAIL
-    else:
-        ok = int(ff.min().item()) == NO_FAIL
-    if rank == 0:  # the gathered canonical secrets are the generated ones
-        ok = ok and bool(torch.equal(last["ys"], splain))
+    g = torch.where(ff == NO_FAIL, ff, ff + sg.start)
+    dist.all_reduce(g, op=dist.ReduceOp.MIN)
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = t.item()
+    checks = {"honest_verdicts": bool((g == NO_FAIL).all().item())}
+    res = None
     if rank == 0:
-        emit({"metric": "secret words/s share+recombine incl. RCCL scatter/gather from one GPU",
-              "value": W * a.steps / el, "unit": "words/s", "n_gpus": world,
-              "steps": a.steps, "warmup": a.warmup, "ms_per_step": el * 1e3 / a.steps,
-              "higher_is_better": True, "scaling": "strong", "verified": ok,
-              "config": {"workload": "C4: root-held arrays scattered over RCCL",
-                         "words_total": W, "parties": n, "parallelism": "dp%d" % world}})
+        # the gathered secrets are the generated ones; the gathered masked
+        # words equal one K_MASK launch over the root's whole arrays
+        checks["secrets_match"] = bool(torch.equal(full_out[1], splain))
+        mo = [tuple(full_in[k * n + j] for k in range(5)) for j in range(n)]
+        ref = torch.empty((W, 16), dtype=torch.uint8, device="cuda")
+        marr, _ = ctx._odo_structs(mo)
+        ff1 = torch.full((1,), NO_FAIL, dtype=torch.int64, device="cuda")
+        assert lib.lib.amph_mask_input(ctx._h, marr, n, full_in[10 * n].data_ptr(), W, ref.data_ptr(),
+                                       C.cast(C.c_void_p(ff1.data_ptr()), C.POINTER(C.c_int64)),
+                                       flags, stream) == 0
+        checks["masked_match_one_gpu"] = bool(torch.equal(full_out[0], ref))
+        moved = sg.moved_bytes()
+        ms = el * 1e3 / a.sg_steps
+        value = W * a.sg_steps / el
+        res = {"words_per_s": value, "ms_per_step": ms, "steps": a.sg_steps, "warmup": a.sg_warmup,
+               "vs_device_resident": round(value / value_resident, 4) if value_resident else None,
+               "root_bytes_per_step": moved, "root_link_GBps": round(moved / (ms * 1e-3) / 1e9, 1),
+               "collective": "RootScatterGather: one batch_isend_irecv group per direction "
+                             "(%s), %d sends per peer each way" % (
+                                 "RCCL ncclSend/ncclRecv over xGMI" if dist.get_backend() == "nccl"
+                                 else dist.get_backend() + " rehearsal, staged through host memory",
+                                 10 * n + 1),
+               "verified": all(checks.values()), "verify_checks": checks}
+    del full_in, full_out, splain
+    return res
 
 
 def host_mode(a, A, torch, ctx, dist=None, rank=0, world=1):
@@ -492,8 +506,27 @@ def dry_run(a, world, rank):
         covered = int(sizes.item())
     else:
         covered = count
+    sg_ok = None
+    if dist.is_initialized() and a.scaling == "strong":
+        # the root-held exchange of scatter_gather_phase on a small array:
+        # one grouped scatter of 10N+1 arrays, a copy standing in for the
+        # kernels, one grouped gather into the root's preallocated output
+        from amphora_amd.shard import RootScatterGather
+        n, Ws = a.parties, 4099
+        sg = RootScatterGather(Ws, 10 * a.parties + 1, 2)
+        full_in = torch.randint(0, 256, (10 * n + 1, Ws, 16), dtype=torch.uint8,
+                                generator=torch.Generator().manual_seed(5)) if rank == 0 else None
+        full_out = torch.zeros((2, Ws, 16), dtype=torch.uint8) if rank == 0 else None
+        local = sg.scatter(full_in)
+        out = sg.out_view(full_out)
+        out[0].copy_(local[0])
+        out[1].copy_(local[10 * n])
+        sg.gather(full_out)
+        if rank == 0:
+            sg_ok = bool(torch.equal(full_out[0], full_in[0]) and torch.equal(full_out[1], full_in[10 * n]))
     if rank == 0:
         emit({"metric": METRIC, "value": None, "unit": "words/s", "n_gpus": world, "dry_run": True,
+              "scatter_gather_round_trip": sg_ok,
               "world_size": world, "backend": dist.get_backend() if dist.is_initialized() else None,
               "scaling": a.scaling, "steps": a.steps, "warmup": a.warmup,
               "words_covered": covered, "fault_reported_at": int(verdicts[-1, 1].item()),
@@ -549,11 +582,6 @@ def main():
     ctx = A.Context(TEST_PRIME, TEST_R, TEST_RINV, device=local)
     if a.mode == "host":
         host_mode(a, A, torch, ctx, dist, rank, world)
-        if distributed:
-            dist.destroy_process_group()
-        return
-    if a.scatter:
-        scatter_mode(a, A, torch, dist, ctx, rank, world)
         if distributed:
             dist.destroy_process_group()
         return
@@ -717,13 +745,35 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "bytes_per_word": bpw, "traffic": traffic},
             "pattern_probe": pattern_probe(probe_ms, n, W, kern),
+            "scatter_gather": None,
             "cpu_baseline": None,
         }
-        if world == 1 and not a.no_cpu_baseline:
+    # The root-held C4 rate (RCCL scatter/gather over xGMI) in the same run,
+    # once the device-resident arrays are gone.
+    resident = total_words * a.steps / el
+    del mask_odos, mbuf, mplain, share_odos, sbuf, splain, secrets, masked, ys, ys2
+    del mviews, sviews, mask_arr, share_arr
+    torch.cuda.empty_cache()
+    sg = None
+    if distributed and a.scaling == "strong" and not a.no_scatter_gather:
+        sg = scatter_gather_phase(a, A, torch, dist, ctx, rank, world, resident)
+        if rank == 0:
+            ok = ok and sg["verified"]
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()  # every collective is done: the other ranks may exit
+    if rank == 0:
+        line["verified"] = ok
+        if sg is not None:
+            line["scatter_gather"] = sg
+        elif a.scaling == "strong" and not a.no_scatter_gather:
+            line["scatter_gather"] = {"skipped": "world size 1: the root's arrays are the only shard, "
+                                                 "nothing crosses a link (device-resident value = "
+                                                 "this point)"}
+        # the CPU baseline on rank 0 at EVERY world size, after the GPU work
+        if not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
         emit(line)
-    if distributed:
-        dist.destroy_process_group()
     if not ok:
         bad = (verdicts != NO_FAIL).any(dim=1).nonzero().flatten().tolist()
         sys.exit("verification failed: checks %r, MAC failures at steps %r" % (checks, bad[:10]))

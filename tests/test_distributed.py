@@ -78,28 +78,108 @@ def test_scatter_verify_gather_two_ranks(tmp_path, W, fault):
     assert int(g) == fault
 
 
-@pytest.mark.parametrize("extra,scaling,words", [([], "strong", 1 << 26),
-                                                  (["--workload", "c2"], "weak", 2 << 20)])
-def test_bench_spawns_ranks_itself(extra, scaling, words):
+@pytest.mark.parametrize("gpus,extra,scaling,words", [(2, [], "strong", 1 << 26),
+                                                       (1, [], "strong", 1 << 26),
+                                                       (2, ["--workload", "c2"], "weak", 2 << 20)])
+def test_bench_spawns_ranks_itself(gpus, extra, scaling, words):
     """`bench.py --gpus 2` with no launcher starts torch.distributed.run as a
     child process (nothing touches a GPU first) and prints ONE JSON line from
     rank 0: n_gpus 2, the C4 workload (2^26 words split into two shards) by
-    default at N > 1, and the verdict all-reduce turns rank 1's local fault
-    index into the global one.  --dry-run: the plumbing without kernels."""
+    default, and the verdict all-reduce turns rank 1's local fault index into
+    the global one; the grouped root scatter/gather round-trips its arrays.
+    The driver's N = 1 default (`bench.py` alone) is the same C4 workload, so
+    BENCH and SCALE measure one curve.  --dry-run: the plumbing without
+    kernels."""
     import json
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--backend", "gloo",
-                        "--same-device", "--dry-run"] + extra,
-                       capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    argv = [sys.executable, os.path.join(root, "bench.py"), "--dry-run"]
+    if gpus > 1:
+        argv += ["--gpus", str(gpus), "--backend", "gloo", "--same-device"]
+    r = subprocess.run(argv + extra, capture_output=True, text=True, timeout=240, env=env, cwd=root)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["backend"] == "gloo"
+    assert line["n_gpus"] == gpus and line["world_size"] == gpus
+    assert line["backend"] == ("gloo" if gpus > 1 else None)
     assert line["scaling"] == scaling and line["words_covered"] == words
     assert line["fault_reported_at"] == line["fault_expected_at"]
     assert line["config"]["workload"].startswith("C4" if scaling == "strong" else "C2")
+    assert line["config"]["words_total"] == words
+    assert line["scatter_gather_round_trip"] is (True if gpus > 1 and scaling == "strong" else None)
+
+
+def _sg_worker(rank, world, port, W, fault, result_dir):
+    """Root holds the 10N+1 C4 input arrays ([mask ODO fields x parties,
+    share ODO fields x parties, secrets]); one grouped scatter, per-shard
+    K_MASK + K_RV arithmetic (the C oracle on CPU here, the HIP kernels in
+    bench.py), one grouped gather of (masked, secrets) into the root's
+    preallocated output -- twice, to show nothing is reallocated."""
+    import torch
+    import torch.distributed as dist
+    from oracle import coracle
+    from amphora_amd.shard import RootScatterGather
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    F = coracle.test_field(threads=1)
+    n = 2
+    sg = RootScatterGather(W, 10 * n + 1, 2)
+    full_in = full_out = None
+    if rank == 0:
+        _, mbuf = F.synth_odos(seed=31, n=n, W=W)
+        _, sbuf = F.synth_odos(seed=32, n=n, W=W, fault_index=fault)
+        sec = F.synth_words(seed=33, count=W, mont=False)
+        full_in = torch.empty((10 * n + 1, W, 16), dtype=torch.uint8)
+        for k in range(5):
+            for j in range(n):
+                full_in[k * n + j] = torch.from_numpy(np.ascontiguousarray(mbuf[k, j]))
+                full_in[5 * n + k * n + j] = torch.from_numpy(np.ascontiguousarray(sbuf[k, j]))
+        full_in[10 * n] = torch.from_numpy(sec)
+        full_out = torch.zeros((2, W, 16), dtype=torch.uint8)
+    ptrs = set()
+    for _ in range(2):
+        local = sg.scatter(full_in)
+        out = sg.out_view(full_out)
+        ptrs.add((local.data_ptr(), out.data_ptr()))
+        ff = [-1, -1]
+        if sg.count:
+            lnp = local.numpy()
+            mo = [tuple(lnp[k * n + j] for k in range(5)) for j in range(n)]
+            so = [tuple(lnp[5 * n + k * n + j] for k in range(5)) for j in range(n)]
+            m, ff[0] = F.mask_input(np.ascontiguousarray(lnp[10 * n]), mo)
+            y, ff[1] = F.recombine_verify(so)
+            out[0].copy_(torch.from_numpy(m))
+            out[1].copy_(torch.from_numpy(y))
+        g = [combine_first_fail(f, sg.start) for f in ff]
+        sg.gather(full_out)
+    if rank == 0:
+        fn = full_in.numpy()
+        mo = [tuple(np.ascontiguousarray(fn[k * n + j]) for k in range(5)) for j in range(n)]
+        so = [tuple(np.ascontiguousarray(fn[5 * n + k * n + j]) for k in range(5)) for j in range(n)]
+        ref_m, ref_mf = F.mask_input(np.ascontiguousarray(fn[10 * n]), mo)
+        ref_y, ref_yf = F.recombine_verify(so)
+        ok = (np.array_equal(full_out[0].numpy(), ref_m) and np.array_equal(full_out[1].numpy(), ref_y)
+              and g == [ref_mf, ref_yf] and len(ptrs) == 1)
+        with open(os.path.join(result_dir, "ok"), "w") as f:
+            f.write("%d %d %d" % (int(ok), g[1], sg.moved_bytes()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W,fault", [(10007, 9001), (4096, -1), (1, -1)])
+def test_root_scatter_gather_grouped_two_ranks(tmp_path, W, fault):
+    """bench.py's root-held C4 exchange (RootScatterGather): gathered masked
+    words and canonical secrets bit-exact with the oracle over the whole
+    array, the verdict min-combined to the global index, no per-step
+    buffers, and exactly rank 1's shard crossing the link each way."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_sg_worker, args=(2, _free_port(), W, fault, str(tmp_path)), nprocs=2,
+                       join=True, start_method="spawn")
+    ok, g, moved = open(tmp_path / "ok").read().split()
+    assert ok == "1"
+    assert int(g) == fault
+    assert int(moved) == (W - (W + 1) // 2) * 23 * 16  # rank 1's shard, 21 arrays out + 2 back
