@@ -64,6 +64,7 @@ def _load():
     L.amph_ctx_destroy.argtypes = [vp]
     L.amph_ctx_device.argtypes = [vp]
     L.amph_ctx_set_batch_words.argtypes = [vp, sz]
+    L.amph_ctx_stats.argtypes = [vp, vp]
     L.amph_strerror.restype = C.c_char_p
     L.amph_strerror.argtypes = [i32]
     L.amph_last_error.restype = C.c_char_p
@@ -74,6 +75,7 @@ def _load():
     L.amph_verify.argtypes = [vp, vp, vp, vp, vp, vp, sz, i64p, u32, vp]
     L.amph_verify_message.argtypes = [vp, vp, vp, vp, vp, vp, C.c_char_p, sz]
     L.amph_mask_words.argtypes = [vp, vp, vp, sz, vp, u32, vp]
+    L.amph_mask_word_host.argtypes = [vp, C.c_char_p, C.c_char_p, vp]
     L.amph_to_gfp.argtypes = [vp, vp, sz, vp, u32, vp]
     L.amph_from_gfp.argtypes = [vp, vp, sz, vp, u32, vp]
     L.amph_convert_share.argtypes = [vp, vp, vp, sz, C.c_char_p, i32, vp, u32, vp]
@@ -116,15 +118,16 @@ def _load():
     L.amph_party_text_dev.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
     L.amph_party_partner_dev.argtypes = [vp, i32, vp, sz, vp, vp]
     L.amph_party_finish_b64_dev.argtypes = [vp, i32, C.POINTER(vp), vp]
+    L.amph_party_reset_partner.argtypes = [vp, i32]
     return L
 
 
 lib = _load()
 
 EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count",
-            "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_set_batch_words", "amph_strerror",
+            "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_set_batch_words", "amph_ctx_stats", "amph_strerror",
             "amph_last_error", "amph_version", "amph_recombine_verify", "amph_mask_input",
-            "amph_recombine", "amph_verify", "amph_verify_message", "amph_mask_words",
+            "amph_recombine", "amph_verify", "amph_verify_message", "amph_mask_words", "amph_mask_word_host",
             "amph_to_gfp", "amph_from_gfp", "amph_convert_share", "amph_odo_pre",
             "amph_open_diffs", "amph_odo_post", "amph_open_post", "amph_synth_odos", "amph_synth_words",
             "amph_host_register", "amph_host_unregister", "amph_time_next_launch",
@@ -135,7 +138,7 @@ EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count",
             "amph_recombine_verify_b64", "amph_mask_input_b64", "amph_party_begin", "amph_party_words", "amph_party_text_len",
             "amph_party_text", "amph_party_partner", "amph_party_finish", "amph_party_finish_b64",
             "amph_party_free", "amph_party_begin_dev", "amph_party_text_dev", "amph_party_partner_dev",
-            "amph_party_finish_b64_dev"]
+            "amph_party_finish_b64_dev", "amph_party_reset_partner"]
 
 
 class TimingEvent:
@@ -161,6 +164,11 @@ class TimingEvent:
 class _AmphOdo(C.Structure):
     _fields_ = [("secret_shares", C.c_void_p), ("r_shares", C.c_void_p), ("v_shares", C.c_void_p),
                 ("w_shares", C.c_void_p), ("u_shares", C.c_void_p), ("nbytes", C.c_size_t)]
+
+
+class _AmphStats(C.Structure):  # amph_stats
+    _fields_ = [(k, C.c_uint64) for k in ("kernel_launches", "pool_buffers", "pool_bytes",
+                                           "device_workers", "worker_tasks")]
 
 
 class _AmphOdoB64(C.Structure):  # amph_odo_b64: one party's five base64 field texts
@@ -229,6 +237,12 @@ class Context:
         if st == AMPH_OK or (allow_verify and st == AMPH_E_VERIFY):
             return st
         raise AmphoraNativeError(st, lib.amph_last_error().decode())
+
+    def stats(self) -> dict:
+        """amph_ctx_stats: kernel launches, pooled party buffers, device workers."""
+        st = _AmphStats()
+        self._check(lib.amph_ctx_stats(self._h, C.byref(st)))
+        return {k: int(getattr(st, k)) for k, _ in _AmphStats._fields_}
 
     def set_batch_words(self, words: int):
         self._check(lib.amph_ctx_set_batch_words(self._h, words))
@@ -704,6 +718,10 @@ class PartySession:
         arr = (C.c_void_p * 5)(*[_ptr(o) for o in outs])
         Context._check(lib.amph_party_finish_b64(self._h, int(is_player0), arr))
         return [o[:nc].tobytes() for o in outs]
+
+    def reset_partner(self, slot: int):
+        """amph_party_reset_partner: free a slot whose text was rejected."""
+        Context._check(lib.amph_party_reset_partner(self._h, slot))
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:

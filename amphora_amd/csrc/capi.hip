@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include <atomic>
 #include <memory>
 #include <thread>
 
@@ -129,6 +130,8 @@ struct amph_ctx {
   hipStream_t streams[kSlots] = {};  // host path: HtoD, kernels, DtoH
   Slot slots[kSlots];
   std::vector<amph_ctx*> sub;  // amph_ctx_create_multi: one context per device
+  // a sub-context's own long-lived thread (run_sharded posts its shards here)
+  std::unique_ptr<amph::DeviceWorker> worker;
   DevBuf ff;  // per-batch first-fail words (host path)
   DevBuf tail;  // small scratch for the partial last unit of codec calls
   DevBuf wire;  // host-mode staging of the wire-text calls (texts, secrets, outputs, verdicts)
@@ -147,9 +150,38 @@ struct amph_ctx {
   // its gigabytes cost tens of microseconds per buffer (hipFree synchronises
   // the device) -- best fit, at most kPartyPoolMax buffers, freed with the context
   std::vector<DevBuf> party_pool;
+  size_t pool_cap_bytes = (size_t)32 << 30;  // AMPH_PARTY_POOL_BYTES
+  std::atomic<uint64_t> launches{0};      // amph_ctx_stats
+  std::atomic<uint64_t> worker_tasks{0};
 };
 
 namespace {
+
+// ---- device memory ------------------------------------------------------------
+// (c->mu held) the party-session buffers pooled for reuse are the only device
+// memory a context keeps that nothing is using: every allocation of the
+// context that runs out of memory frees them and tries once more, so the
+// pool never causes the out-of-memory error it would then report.
+size_t pool_bytes(const amph_ctx* c) {
+  size_t t = 0;
+  for (const DevBuf& b : c->party_pool) t += b.cap;
+  return t;
+}
+
+void pool_reclaim(amph_ctx* c) {
+  for (DevBuf& b : c->party_pool) b.release();
+  c->party_pool.clear();
+}
+
+hipError_t dev_ensure(amph_ctx* c, DevBuf& b, size_t bytes) {
+  hipError_t e = b.ensure(bytes);
+  if (e == hipErrorOutOfMemory && !c->party_pool.empty()) {
+    (void)hipGetLastError();
+    pool_reclaim(c);
+    e = b.ensure(bytes);
+  }
+  return e;
+}
 
 // ---- field setup (host) -----------------------------------------------------
 u128 add_mod(u128 a, u128 b, u128 p) {  // a, b < p
@@ -198,6 +230,7 @@ int block_for(const amph_ctx* c, size_t words) {
 }
 
 amph::LaunchCfg cfg(amph_ctx* c, hipStream_t s, size_t words) {
+  c->launches.fetch_add(1, std::memory_order_relaxed);
   amph::LaunchCfg lc{s, c->grid_cap, block_for(c, words)};
   lc.ev_start = g_ev_start;  // consumed by this launch only
   lc.ev_stop = g_ev_stop;
@@ -337,13 +370,13 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
     if (!out_pinned[k]) hout_bytes += align256(bw * outs[k].bytes_per_word);
   }
   for (int s = 0; s < S && (size_t)s < nb; ++s) {
-    hipError_t e = c->slots[s].dev.ensure(dev_bytes);
+    hipError_t e = dev_ensure(c, c->slots[s].dev, dev_bytes);
     if (e == hipSuccess) e = c->slots[s].hin.ensure(hin_bytes);
     if (e == hipSuccess) e = c->slots[s].hout.ensure(hout_bytes);
     if (e != hipSuccess) return fail(AMPH_E_NOMEM, std::string("batch buffers: ") + hipGetErrorString(e));
   }
   if (with_ff) {
-    hipError_t e = c->ff.ensure(nb * sizeof(unsigned long long));
+    hipError_t e = dev_ensure(c, c->ff, nb * sizeof(unsigned long long));
     if (e != hipSuccess) return fail(AMPH_E_NOMEM, "first-fail words");
     HIP_TRY(hipMemsetAsync(c->ff.p, 0x7F, nb * sizeof(unsigned long long), s_k));
   }
@@ -480,7 +513,7 @@ bool small_call(const amph_ctx* c, size_t bytes) { return c->small_bytes && byte
 // device verdict words, reset if an earlier call left them unknown
 int small_begin(amph_ctx* c, size_t bytes, hipStream_t s, Arena* a, unsigned long long** dff) {
   if (c->small.ensure(bytes + 256) != hipSuccess) return fail(AMPH_E_NOMEM, "small-call arena");
-  if (c->small_ff.ensure(256) != hipSuccess) return fail(AMPH_E_NOMEM, "small-call verdict words");
+  if (dev_ensure(c, c->small_ff, 256) != hipSuccess) return fail(AMPH_E_NOMEM, "small-call verdict words");
   if (c->small_ff_dirty) {
     HIP_TRY(hipMemsetAsync(c->small_ff.p, 0x7F, 256, s));
     c->small_ff_dirty = false;
@@ -590,15 +623,17 @@ int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
     std::string err;
   };
   std::vector<Res> res(nd);
-  std::vector<std::thread> th;
-  for (size_t d = 0; d < nd && d * per < words; ++d) {
+  size_t used = 0;
+  while (used < nd && used * per < words) ++used;
+  amph::Latch done(used);
+  for (size_t d = 0; d < used; ++d) {
     const size_t start = d * per, cnt = std::min(per, words - start);
     std::vector<HostIn> in2(ins);
     for (auto& x : in2) x.host += start * x.bytes_per_word;
     std::vector<HostOut> out2(outs);
     for (auto& x : out2) x.host += start * x.bytes_per_word;
-    th.emplace_back([&, d, cnt, in2 = std::move(in2), out2 = std::move(out2)]() {
-      amph_ctx* s = g->sub[d];
+    amph_ctx* s = g->sub[d];
+    s->worker->post([&, d, s, cnt, in2 = std::move(in2), out2 = std::move(out2)]() {
       try {
         std::lock_guard<std::mutex> lk(s->mu);
         res[d].st = run_batched(s, cnt, in2, out2, with_ff, &res[d].ff, launch, ff_scale);
@@ -606,12 +641,14 @@ int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
         res[d].st = fail(AMPH_E_NOMEM, e.what());
       }
       if (res[d].st != AMPH_OK) res[d].err = g_last_error;
+      s->worker_tasks.fetch_add(1, std::memory_order_relaxed);
+      done.count_down();
     });
   }
-  for (auto& t : th) t.join();
-  for (size_t d = 0; d < th.size(); ++d)
+  done.wait();
+  for (size_t d = 0; d < used; ++d)
     if (res[d].st != AMPH_OK && res[d].st != AMPH_E_VERIFY) return fail(res[d].st, res[d].err);
-  for (size_t d = 0; d < th.size(); ++d)
+  for (size_t d = 0; d < used; ++d)
     if (res[d].st == AMPH_E_VERIFY) {
       if (first_fail) *first_fail = (int64_t)(d * per * ff_scale) + res[d].ff;
       return AMPH_E_VERIFY;
@@ -743,8 +780,10 @@ int amph_ctx_create(const uint8_t p_le[16], const uint8_t r_le[16], const uint8_
     return st;
   }
   c->device = device;
+  c->small.flags = hipHostMallocCoherent;  // kernels read and write the arena in place
   if (const char* g = std::getenv("AMPH_GRID_CAP")) c->grid_cap = std::max(0, std::atoi(g));
   if (const char* sb = std::getenv("AMPH_SMALL_BYTES")) c->small_bytes = (size_t)std::strtoull(sb, nullptr, 10);
+  if (const char* pb = std::getenv("AMPH_PARTY_POOL_BYTES")) c->pool_cap_bytes = (size_t)std::strtoull(pb, nullptr, 10);
   if (const char* b = std::getenv("AMPH_BLOCK")) {
     const int v = std::atoi(b);
     if (v >= 64 && v <= amph::kMaxBlock && v % 64 == 0) c->block = v;
@@ -767,7 +806,12 @@ int amph_ctx_create_multi(const uint8_t p_le[16], const uint8_t r_le[16],
       amph_ctx_destroy(g);
       return st;
     }
+    s->worker.reset(new (std::nothrow) amph::DeviceWorker());
     g->sub.push_back(s);
+    if (!s->worker) {
+      amph_ctx_destroy(g);
+      return fail(AMPH_E_NOMEM, "device worker thread");
+    }
   }
   *out = g;
   return AMPH_OK;
@@ -779,6 +823,7 @@ int amph_ctx_device_count(const amph_ctx* c) {
 
 void amph_ctx_destroy(amph_ctx* c) {
   if (!c) return;
+  c->worker.reset();  // drains its queue and joins: nothing of c runs after this
   for (amph_ctx* s : c->sub) amph_ctx_destroy(s);
   c->sub.clear();
   if (c->streams[0] || c->slots[0].dev.p || c->ff.p) {
@@ -817,6 +862,23 @@ void amph_ctx_destroy(amph_ctx* c) {
 }
 
 int amph_ctx_device(const amph_ctx* c) { return c ? c->device : -1; }
+
+int amph_ctx_stats(amph_ctx* c, amph_stats* out) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (!out) return fail(AMPH_E_PARAM, "null stats output");
+  *out = amph_stats{};
+  auto add = [&](amph_ctx* x) {
+    std::lock_guard<std::mutex> g(x->mu);
+    out->kernel_launches += x->launches.load(std::memory_order_relaxed);
+    out->pool_buffers += x->party_pool.size();
+    out->pool_bytes += pool_bytes(x);
+    out->device_workers += x->worker ? 1 : 0;
+    out->worker_tasks += x->worker_tasks.load(std::memory_order_relaxed);
+  };
+  add(c);
+  for (amph_ctx* s : c->sub) add(s);
+  return AMPH_OK;
+}
 
 int amph_ctx_set_batch_words(amph_ctx* c, size_t words) {
   if (check_ctx(c)) return AMPH_E_PARAM;
@@ -1198,6 +1260,17 @@ int amph_mask_words(amph_ctx* c, const uint8_t* secrets, const uint8_t* masks, s
                      });
 }
 
+int amph_mask_word_host(amph_ctx* c, const uint8_t secret[16], const uint8_t mask[16], uint8_t out[16]) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  if (!secret || !mask || !out) return fail(AMPH_E_PARAM, "null word");
+  const u128 s = ld128(secret) % c->p, m = ld128(mask) % c->p;
+  u128 d = s - m;  // mod 2^128; the true difference (s - m) mod p is < p < 2^128
+  if (s < m) d += c->p;
+  const W4 x = amph::mont_mul(w4_of(d), amph::r2_word(c->f), c->f);  // d R mod p, reduced
+  for (int i = 0; i < 4; ++i) std::memcpy(out + 4 * i, &x.v[i], 4);
+  return AMPH_OK;
+}
+
 // ---- base64 wire codec ---------------------------------------------------------
 }  // extern "C"
 namespace {
@@ -1210,7 +1283,7 @@ template <class Launch>
 int run_tail(amph_ctx* c, const void* in, size_t in_bytes, void* out, size_t out_bytes,
              bool with_bad, unsigned long long* bad_host, Launch&& launch) {
   HIP_TRY(use_device(c->device));
-  hipError_t e = c->tail.ensure(512);
+  hipError_t e = dev_ensure(c, c->tail, 512);
   if (e != hipSuccess) return fail(AMPH_E_NOMEM, "tail scratch");
   if (!c->streams[0]) HIP_TRY(hipStreamCreateWithFlags(&c->streams[0], hipStreamNonBlocking));
   hipStream_t s = c->streams[0];  // the context's own stream: no device-wide sync
@@ -1371,7 +1444,7 @@ int dev_scratch(amph_ctx* c, size_t bytes, hipStream_t s, void** p) {
   else HIP_TRY(hipStreamWaitEvent(s, c->xdev_done, 0));
   if (c->xdev.cap < bytes) {
     HIP_TRY(hipEventSynchronize(c->xdev_done));  // the old buffer is idle before it is freed
-    if (c->xdev.ensure(bytes) != hipSuccess) return fail(AMPH_E_NOMEM, "exchange scratch");
+    if (dev_ensure(c, c->xdev, bytes) != hipSuccess) return fail(AMPH_E_NOMEM, "exchange scratch");
   }
   *p = c->xdev.p;
   return AMPH_OK;
@@ -1394,7 +1467,7 @@ struct XStage {
   int stage(amph_ctx* c, const size_t* sizes, int n) {
     size_t total = 0;
     for (int i = 0; i < n; ++i) total += align256(sizes[i] ? sizes[i] : 16);
-    hipError_t e = c->xstage.ensure(total);
+    hipError_t e = dev_ensure(c, c->xstage, total);
     if (e != hipSuccess) return fail(AMPH_E_NOMEM, "exchange staging");
     base = (uint8_t*)c->xstage.p;
     return AMPH_OK;
@@ -1621,7 +1694,7 @@ struct WireHost {
       base = a.base;
       off = a.off;
     } else {
-      hipError_t e = c->wire.ensure(bytes);
+      hipError_t e = dev_ensure(c, c->wire, bytes);
       if (e != hipSuccess) return fail(AMPH_E_NOMEM, "wire staging");
       base = (uint8_t*)c->wire.p;
     }
@@ -1865,6 +1938,7 @@ struct amph_party {
   uint64_t* enc_lens = nullptr;  // K_ODO_PRE's exchange text lengths, scanned by the encode
   uint64_t text_len = 0;
   uint32_t have = 0;  // bit j: party j's diffs are on the device (bit 0 after begin)
+  const unsigned long long* bad_dev[AMPH_MAX_PARTIES] = {};  // device mode: partner verdict words
   bool finished = false;
   ~amph_party() {
     mem.release();
@@ -1879,13 +1953,15 @@ size_t b64_chars(size_t nbytes) { return 4 * ((nbytes + 2) / 3); }
 
 constexpr size_t kPartyPoolMax = 16;
 
-// (c->mu held) hand a session buffer back to the context's pool
+// (c->mu held) hand a session buffer back to the context's pool: at most
+// kPartyPoolMax buffers and c->pool_cap_bytes bytes, the smallest dropped first
 void pool_put(amph_ctx* c, DevBuf& b) {
   if (!b.p) return;
   c->party_pool.push_back(b);
   b.p = nullptr;
   b.cap = 0;
-  while (c->party_pool.size() > kPartyPoolMax) {  // drop the smallest
+  while (!c->party_pool.empty() &&
+         (c->party_pool.size() > kPartyPoolMax || pool_bytes(c) > c->pool_cap_bytes)) {
     size_t m = 0;
     for (size_t i = 1; i < c->party_pool.size(); ++i)
       if (c->party_pool[i].cap < c->party_pool[m].cap) m = i;
@@ -1895,7 +1971,7 @@ void pool_put(amph_ctx* c, DevBuf& b) {
 }
 
 // (c->mu held) b holds at least `bytes`: kept, or the best-fitting pooled
-// buffer, or a new allocation
+// buffer, or a new allocation (after freeing the pool if memory ran out)
 hipError_t pool_ensure(amph_ctx* c, DevBuf& b, size_t bytes) {
   if (bytes <= b.cap) return hipSuccess;
   pool_put(c, b);
@@ -1908,7 +1984,7 @@ hipError_t pool_ensure(amph_ctx* c, DevBuf& b, size_t bytes) {
     c->party_pool.erase(c->party_pool.begin() + best);
     return hipSuccess;
   }
-  return b.ensure(bytes);
+  return dev_ensure(c, b, bytes);
 }
 
 int party_check(amph_party* p) {
@@ -2221,6 +2297,17 @@ int amph_party_partner_dev(amph_party* p, int slot, const char* text, size_t len
   p->dstream = (hipStream_t)stream;
   if (int st = party_decode(p, slot, text, len, (unsigned long long*)bad_index, p->dstream)) return st;
   p->have |= 1u << slot;
+  p->bad_dev[slot] = (const unsigned long long*)bad_index;
+  return AMPH_OK;
+}
+
+int amph_party_reset_partner(amph_party* p, int slot) {
+  if (int st = party_check(p)) return st;
+  if (slot < 1 || slot >= p->n)
+    return fail(AMPH_E_PARAM, "partner slot must be in [1, " + std::to_string(p->n - 1) + "]");
+  std::lock_guard<std::mutex> g(p->c->mu);
+  p->have &= ~(1u << slot);
+  p->bad_dev[slot] = nullptr;
   return AMPH_OK;
 }
 
@@ -2234,6 +2321,12 @@ int amph_party_finish_b64_dev(amph_party* p, int is_player0, const char* fields_
   p->dstream = (hipStream_t)stream;
   if (int st = party_open_post(p, is_player0, p->dstream)) return st;
   if (int st = party_b64(p, p->dstream)) return st;
+  amph::PoisonB64 pz{};
+  for (int j = 1; j < p->n; ++j)
+    if (p->bad_dev[j]) pz.bad[pz.n_bad++] = p->bad_dev[j];
+  for (int k = 0; k < 5; ++k) pz.field[k] = p->b64[k];
+  pz.chars = b64_chars(16 * p->W);
+  if (hipError_t e = amph::launch_poison_b64(pz, p->dstream)) return hip_fail(e, "k_poison_b64");
   for (int k = 0; k < 5; ++k) fields_b64[k] = p->b64[k];
   p->finished = true;
   return AMPH_OK;

@@ -14,6 +14,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -24,10 +25,15 @@ namespace amph {
 struct PinnedBuf {
   void* p = nullptr;
   size_t cap = 0;
+  // hipHostMallocDefault for DMA staging (only the copy engines touch it);
+  // hipHostMallocCoherent for memory kernels read and write in place
+  // (run_small's arena): fine-grained, so a kernel never sees a line its
+  // device cached from an earlier call at the same address.
+  unsigned flags = hipHostMallocDefault;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
     release();
-    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, bytes, flags);
     if (e == hipSuccess) cap = bytes;
     else p = nullptr;
     return e;
@@ -116,6 +122,74 @@ class CopyPool {
   size_t remaining_ = 0;
   size_t gen_ = 0;
   bool stop_ = false;
+};
+
+// One long-lived thread that owns a device for a multi-device context's
+// sub-context: run_sharded posts each call's shard to it instead of starting
+// a fresh std::thread per call (a fresh thread's first HIP call pays the
+// runtime's per-thread device setup, ~76 us of hipSetDevice in
+// profiles/r03_c1_rocprof_before_pool.txt, on every call).  Tasks run in
+// post order; the destructor drains the queue and joins.
+class DeviceWorker {
+ public:
+  DeviceWorker() : th_([this] { loop(); }) {}
+  ~DeviceWorker() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  DeviceWorker(const DeviceWorker&) = delete;
+  DeviceWorker& operator=(const DeviceWorker&) = delete;
+  void post(std::function<void()> fn) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(std::move(fn));
+    }
+    cv_.notify_one();
+  }
+  std::thread::id id() const { return th_.get_id(); }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> fn;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        fn = std::move(q_.front());
+        q_.pop_front();
+      }
+      fn();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  bool stop_ = false;
+  std::thread th_;  // last: starts once the members above exist
+};
+
+// Completion count for a fan-out over DeviceWorkers.
+class Latch {
+ public:
+  explicit Latch(size_t n) : n_(n) {}
+  void count_down() {
+    std::lock_guard<std::mutex> g(m_);
+    if (--n_ == 0) cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(m_);
+    cv_.wait(lk, [&] { return n_ == 0; });
+  }
+
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  size_t n_;
 };
 
 inline bool is_pinned_host(const void* p) {

@@ -1125,6 +1125,26 @@ __global__ void k_take_words(unsigned long long* dev, unsigned long long* host, 
 }
 }  // namespace
 
+namespace {
+// Device-mode party session (capi.hip amph_party_finish_b64_dev): if any
+// partner text's verdict word reports a failure, the five base64 fields are
+// made unusable -- their first unit becomes "!!!!", which no base64 decoder
+// accepts -- so a response sent without checking the verdicts cannot carry
+// values computed from a rejected text.
+__global__ void k_poison_b64(PoisonB64 a) {
+  bool bad = false;
+  for (int i = 0; i < a.n_bad; ++i) bad |= *a.bad[i] != kNoFail;
+  const int t = threadIdx.x;
+  if (bad && t < 20) a.field[t / 4][t % 4] = '!';
+}
+}  // namespace
+
+hipError_t launch_poison_b64(const PoisonB64& a, hipStream_t s) {
+  if (a.n_bad <= 0 || a.chars < 4) return hipSuccess;
+  hipLaunchKernelGGL(k_poison_b64, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_take_words(unsigned long long* dev, unsigned long long* host, int n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_take_words, dim3(1), dim3(64), 0, s, dev, host, n);

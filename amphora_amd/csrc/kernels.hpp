@@ -182,6 +182,16 @@ hipError_t launch_mask_b64(const TextSet& tx, int n, size_t words, size_t nchars
 // host memory and reset them to kNoFail (one 64-lane workgroup).
 hipError_t launch_take_words(unsigned long long* dev, unsigned long long* host, int n, hipStream_t s);
 
+// Device-mode party session: poison the five base64 fields ("!!!!" as their
+// first unit) when any partner verdict word is not kNoFail (one workgroup).
+struct PoisonB64 {
+  const unsigned long long* bad[16];
+  int n_bad;
+  char* field[5];
+  size_t chars;  // characters per field
+};
+hipError_t launch_poison_b64(const PoisonB64& a, hipStream_t s);
+
 // Measurement only: K_MASK's memory pattern without the arithmetic.
 hipError_t launch_stream_probe(const OdoSet& odo, int n, size_t words, const uint4* secrets,
                                uint4* out, const LaunchCfg& c);

@@ -136,6 +136,27 @@ int amph_ctx_device_count(const amph_ctx* ctx);
  * threads (AMPH_HOST_THREADS, default min(8, cores/2)) with HtoD, kernel and
  * DtoH of consecutive batches overlapped on 3 HIP streams. */
 int amph_ctx_set_batch_words(amph_ctx* ctx, size_t words);
+
+/* Counters of a context (summed over the devices of a multi-device context),
+ * for tests and operators: no reference interface corresponds (the Java
+ * path has no device state).
+ *   kernel_launches  arithmetic / codec kernels launched so far
+ *   pool_buffers / pool_bytes  party-session device buffers kept for reuse
+ *     after amph_party_free (at most 16 buffers and AMPH_PARTY_POOL_BYTES
+ *     bytes, default 32 GiB, per device; freed, and the allocation retried,
+ *     when any device allocation of the context runs out of memory)
+ *   device_workers   long-lived per-device threads of a multi-device
+ *     context (created with it; run_sharded posts each call's shards to
+ *     them instead of starting threads per call)
+ *   worker_tasks     shards those workers have run */
+typedef struct amph_stats {
+  uint64_t kernel_launches;
+  uint64_t pool_buffers;
+  uint64_t pool_bytes;
+  uint64_t device_workers;
+  uint64_t worker_tasks;
+} amph_stats;
+int amph_ctx_stats(amph_ctx* ctx, amph_stats* out);
 /* Page-lock a caller buffer (hipHostRegister, portable to every device) so
  * host-pointer calls DMA it directly without the staging copy (e.g. a
  * long-lived direct ByteBuffer). */
@@ -205,6 +226,13 @@ int amph_verify_message(amph_ctx* ctx, const uint8_t y[16], const uint8_t r[16],
  * out[i] = toGfp((secrets[i] - masks[i]) mod p); both LE16 integers. */
 int amph_mask_words(amph_ctx* ctx, const uint8_t* secrets, const uint8_t* masks, size_t words,
                     uint8_t* out, uint32_t flags, void* stream);
+/* The same for ONE word on the calling thread, with no device work: the
+ * reference's per-word maskInput (SecretShareUtil.java:65-68, called once per
+ * word by DefaultAmphoraClient.java:155-160) is not worth a kernel launch and
+ * a stream synchronisation.  secret / mask are LE16 integers (reduced mod p
+ * here); out = LE16((secret - mask) mod p * R mod p).  Batched callers use
+ * amph_mask_input (verify + mask on the GPU). */
+int amph_mask_word_host(amph_ctx* ctx, const uint8_t secret[16], const uint8_t mask[16], uint8_t out[16]);
 
 /* MpSpdzIntegrationUtils.toGfp / fromGfp over word arrays (mp-spdz-integration
  * 0.2.2, absent; restated): toGfp(x) = LE16(x R mod p) for any LE16 integer x;
@@ -418,9 +446,15 @@ void amph_party_free(amph_party* party);
  * finishing.  finish_b64_dev: the five fields as base64 text in the session's
  * device memory, *fields_b64[k] their addresses (amph_party_finish_b64's
  * lengths; valid until amph_party_free) -- the response is sent from there.
+ * If any partner's *bad_index reports a failure when finish_b64_dev's
+ * kernels run, the five fields come out poisoned: their first four
+ * characters are "!!!!" (no base64 decoder accepts them), so a response sent
+ * without checking the verdicts cannot carry values computed from a rejected
+ * text.  To resubmit a slot whose text was rejected, amph_party_reset_partner
+ * it first (same stream, or after synchronising).
  * A device-mode session takes only these calls (and amph_party_words /
- * amph_party_free; amph_party_text_len reads 0 for it -- its length is the
- * device word); a multi-device context is refused. */
+ * amph_party_reset_partner / amph_party_free; amph_party_text_len reads 0 for
+ * it -- its length is the device word); a multi-device context is refused. */
 int amph_party_begin_dev(amph_ctx* ctx, const uint8_t* share_data, size_t share_stride,
                          const uint8_t* mask_tuples, const uint8_t* triples, size_t words, int n_parties,
                          uint8_t* out_y, uint8_t* out_r, uint8_t* out_v, void* stream, amph_party** out);
@@ -428,6 +462,9 @@ int amph_party_text_dev(amph_party* party, const char** text, const uint64_t** t
 int amph_party_partner_dev(amph_party* party, int slot, const char* text, size_t len, int64_t* bad_index,
                            void* stream);
 int amph_party_finish_b64_dev(amph_party* party, int is_player0, const char* fields_b64[5], void* stream);
+/* Frees partner slot `slot` (1 .. n_parties-1) of an unfinished session
+ * (either mode) for another amph_party_partner(_dev) call. */
+int amph_party_reset_partner(amph_party* party, int slot);
 
 /* ---- benchmark / test input generation (device pointers only) ---------- */
 /* Honest n-party ODOs: out_fields[k * n_parties + j] = field k (y,r,v,w,u) of

@@ -48,6 +48,12 @@ final class NativeShareArithmetic {
   /** maskInput over canonical LE16 secrets and masks: toGfp((s - m) mod p) per word */
   static native void maskWords(long ctx, byte[] secretsLe, byte[] masksLe, byte[] outMasked);
 
+  /**
+   * maskInput for ONE word (SecretShareUtil.java:65-68): host arithmetic in libamphora_hip, no
+   * kernel launch (amph_mask_word_host); the batch path is maskInput above
+   */
+  static native byte[] maskWord(long ctx, byte[] secretLe, byte[] maskLe);
+
   static native String verifyMessage(long ctx, byte[] y, byte[] r, byte[] u, byte[] v, byte[] w);
 
   /** getSecret from the five base64 strings per party (ASCII): -1 or the failing word */

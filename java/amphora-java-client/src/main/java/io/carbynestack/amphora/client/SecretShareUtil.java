@@ -64,15 +64,20 @@ class SecretShareUtil implements AutoCloseable {
     }
   }
 
-  /** maskInput :65-68: MaskedInputData.of(toGfp((secret - inputMask) mod p)) */
+  /**
+   * maskInput :65-68: MaskedInputData.of(toGfp((secret - inputMask) mod p)).
+   *
+   * <p>One word: computed on the calling thread (amph_mask_word_host), with no kernel launch and
+   * no stream synchronisation, so the unpatched DefaultAmphoraClient's per-word parallel loop
+   * (:155-160) costs what the BigInteger code did. The GPU path for a whole secret is {@link
+   * #maskInputs} (java/patches/DefaultAmphoraClient.patch).
+   */
   MaskedInputData maskInput(BigInteger secret, BigInteger inputMask) {
     byte[] s = new byte[WORD_WIDTH];
     byte[] m = new byte[WORD_WIDTH];
-    byte[] out = new byte[WORD_WIDTH];
     NativeShareArithmetic.putWord(secret, prime, s, 0);
     NativeShareArithmetic.putWord(inputMask, prime, m, 0);
-    NativeShareArithmetic.maskWords(ctx, s, m, out);
-    return MaskedInputData.of(out);
+    return MaskedInputData.of(NativeShareArithmetic.maskWord(ctx, s, m));
   }
 
   /** recombineObject :70-90: word i = sum over the shares of fromGfp(word i) mod p */

@@ -32,13 +32,29 @@ public class SecretShareUtil implements AutoCloseable {
   @Autowired
   public SecretShareUtil(MpSpdzIntegrationUtils spdzUtil) {
     this.prime = spdzUtil.getPrime();
-    this.ctx = createContext(prime);
+    this.ctx = createContext(spdzUtil);
   }
 
-  /** the context for the field: r = 2^128 mod p, rInv = r^-1 mod p (MP-SPDZ's auxiliary modulus) */
-  static long createContext(BigInteger prime) {
-    BigInteger r = BigInteger.ONE.shiftLeft(128).mod(prime);
-    return NativeShareArithmetic.ctxCreate(le16(prime), le16(r), le16(r.modInverse(prime)), devices());
+  /**
+   * The context for the CONFIGURED field (UtilsConfig.java:17-20: SpdzProperties prime, r, rInv):
+   * r and rInv are read back from the configured codec itself -- toGfp(1) = r mod p and
+   * fromGfp(word 1) = rInv mod p under the Montgomery encoding -- not recomputed, so a deployment
+   * whose r is not 2^128 mod p is refused by amph_ctx_create ("r must equal 2^128 mod prime")
+   * instead of silently diverging from the reference.
+   */
+  static long createContext(MpSpdzIntegrationUtils spdzUtil) {
+    BigInteger prime = spdzUtil.getPrime();
+    byte[] one = new byte[WORD_WIDTH];
+    one[0] = 1;
+    BigInteger r = leInt(spdzUtil.toGfp(BigInteger.ONE));
+    BigInteger rInv = spdzUtil.fromGfp(one);
+    return NativeShareArithmetic.ctxCreate(le16(prime), le16(r), le16(rInv), devices());
+  }
+
+  static BigInteger leInt(byte[] le) {
+    byte[] be = new byte[le.length];
+    for (int k = 0; k < le.length; k++) be[k] = le[le.length - 1 - k];
+    return new BigInteger(1, be);
   }
 
   @Override

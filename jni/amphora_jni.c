@@ -249,6 +249,28 @@ JNIEXPORT void JNICALL CLIENT(maskWords)(JNIEnv* env, jclass cls, jlong ctx, jby
   if (st != AMPH_OK) throw_status(env, st);
 }
 
+/* SecretShareUtil.maskInput :65-68 for ONE word, as DefaultAmphoraClient.java:155-160 calls it:
+   16-byte region copies in and out (no critical region) and host arithmetic in
+   libamphora_hip (amph_mask_word_host) -- no kernel launch per word */
+JNIEXPORT jbyteArray JNICALL CLIENT(maskWord)(JNIEnv* env, jclass cls, jlong ctx, jbyteArray secret,
+                                              jbyteArray mask) {
+  (void)cls;
+  Pin a[2];
+  if (ref(env, secret, &a[0]) || ref(env, mask, &a[1])) return NULL;
+  if (a[0].len != 16 || a[1].len != 16) return throw_arg(env, "maskWord takes two 16-byte words"), NULL;
+  jbyte s[16], m[16], o[16];
+  (*env)->GetByteArrayRegion(env, secret, 0, 16, s);
+  (*env)->GetByteArrayRegion(env, mask, 0, 16, m);
+  const int st = amphj_mask_word(CTX(ctx), (const uint8_t*)s, (const uint8_t*)m, (uint8_t*)o);
+  if (st != AMPH_OK) {
+    throw_status(env, st);
+    return NULL;
+  }
+  jbyteArray out = (*env)->NewByteArray(env, 16);
+  if (out) (*env)->SetByteArrayRegion(env, out, 0, 16, o);
+  return out;
+}
+
 /* the IntegrityVerificationException text of SecretShareUtil.java:116-129 */
 JNIEXPORT jstring JNICALL CLIENT(verifyMessage)(JNIEnv* env, jclass cls, jlong ctx, jbyteArray y, jbyteArray r,
                                                 jbyteArray u, jbyteArray v, jbyteArray w) {

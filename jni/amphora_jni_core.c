@@ -126,6 +126,10 @@ int amphj_mask_words(void* ctx, const uint8_t* secrets, size_t s_len, const uint
   return abi(amph_mask_words((amph_ctx*)ctx, secrets, masks, W, out, 0, NULL));
 }
 
+int amphj_mask_word(void* ctx, const uint8_t secret[16], const uint8_t mask[16], uint8_t out[16]) {
+  return abi(amph_mask_word_host((amph_ctx*)ctx, secret, mask, out));
+}
+
 int amphj_verify_message(void* ctx, const uint8_t* y, const uint8_t* r, const uint8_t* u,
                          const uint8_t* v, const uint8_t* w, char* buf, size_t cap) {
   const int len = amph_verify_message((amph_ctx*)ctx, y, r, u, v, w, buf, cap);

@@ -50,6 +50,8 @@ int amphj_recombine(void* ctx, int n, const uint8_t* const* shares, const size_t
 int amphj_verify(void* ctx, const uint8_t* const* ys_rs_us_vs_ws, const size_t* lens, int64_t* fail);
 int amphj_mask_words(void* ctx, const uint8_t* secrets, size_t s_len, const uint8_t* masks,
                      size_t m_len, uint8_t* out, size_t out_len);
+/* one word on the calling thread (amph_mask_word_host): no device work */
+int amphj_mask_word(void* ctx, const uint8_t secret[16], const uint8_t mask[16], uint8_t out[16]);
 /* the IntegrityVerificationException text for one word (5 LE16 values) */
 int amphj_verify_message(void* ctx, const uint8_t* y, const uint8_t* r, const uint8_t* u,
                          const uint8_t* v, const uint8_t* w, char* buf, size_t cap);

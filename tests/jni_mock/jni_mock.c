@@ -33,6 +33,7 @@ static int g_local;          /* local references made in this native call */
 static int g_capacity = 16;  /* the JNI guarantee, or what EnsureLocalCapacity reserved */
 static int g_ref_overflows;  /* local references beyond it */
 static int g_fail_pin;       /* > 0: the g_fail_pin-th pin from now returns NULL */
+static int g_pins;           /* critical pins taken since mock_clear */
 
 static struct mock_obj* obj_new(int kind, jsize len, size_t elem) {
   struct mock_obj* o = (struct mock_obj*)calloc(1, sizeof *o);
@@ -96,6 +97,7 @@ static void* m_GetPrimitiveArrayCritical(JNIEnv* env, jarray a, jboolean* is_cop
     return NULL;
   }
   ++g_critical;
+  ++g_pins;
   ++a->pinned;
   return a->data;
 }
@@ -190,6 +192,7 @@ JNIEXPORT int mock_violations(void) { return g_violations; }
 JNIEXPORT int mock_open_criticals(void) { return g_critical; }
 JNIEXPORT int mock_ref_overflows(void) { return g_ref_overflows; }
 JNIEXPORT void mock_fail_pin(int k) { g_fail_pin = k; }
+JNIEXPORT int mock_pins(void) { return g_pins; }
 
 JNIEXPORT void mock_clear(void) {
   g_exc_class[0] = g_exc_msg[0] = 0;
@@ -198,6 +201,7 @@ JNIEXPORT void mock_clear(void) {
   g_capacity = 16;
   g_ref_overflows = 0;
   g_fail_pin = 0;
+  g_pins = 0;
 }
 
 JNIEXPORT void mock_free_all(void) {

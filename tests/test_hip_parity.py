@@ -251,11 +251,18 @@ def test_multi_device_context(ctx, F):
     g = A.Context(P, R, RINV, devices=[0, 0, 0])
     g.set_batch_words(8192)  # several batches per shard
     W = 100_003  # shards of 33 335 words
+    # the shards run on the sub-contexts' long-lived workers, not on threads
+    # started per call
+    st0 = g.stats()
+    assert st0["device_workers"] == 3 and st0["worker_tasks"] == 0
     for fault in (-1, 70_000, 33_334, 33_335):
         odos, _ = F.synth_odos(seed=600, n=3, W=W, fault_index=fault, noncanon_permille=10)
         y, ff = g.recombine_verify(odos)
         oy, off = F.recombine_verify(odos)
         assert ff == off == fault and np.array_equal(y, oy), fault
+    st1 = g.stats()
+    assert st1["device_workers"] == 3 and st1["worker_tasks"] == 3 * 4
+    assert st1["kernel_launches"] >= 3 * 4
     # two faults in different shards: the smaller index wins
     odos, _ = F.synth_odos(seed=601, n=2, W=W, fault_index=90_000)
     odos[1][4][40_000, 0] ^= 1
@@ -542,3 +549,21 @@ def test_host_verdicts_follow_the_kernels(ctx, F):
             assert ctx.mask_input(odos, secrets)[1] == W - 1
     finally:
         ctx.set_batch_words(4 << 20)
+
+
+def test_small_calls_back_to_back_same_addresses(ctx, F):
+    """the small-call arena (run_small) is read and written in
+    place by the kernels at the same addresses on every call; many calls in
+    a row with different inputs must each see their own inputs (the arena is
+    fine-grained / coherent host memory, so no line cached by an earlier
+    call is served).  Every result is compared with the oracle."""
+    W = 500  # well under AMPH_SMALL_BYTES: every call takes the small path
+    for i in range(60):
+        odos, _ = F.synth_odos(seed=7000 + i, n=2, W=W, fault_index=(i * 37) % W if i % 3 == 0 else -1)
+        secrets = F.synth_words(seed=8000 + i, count=W, mont=False)
+        y, ff = ctx.recombine_verify(odos)
+        oy, off = F.recombine_verify(odos)
+        assert ff == off and np.array_equal(y, oy), i
+        m, mf = ctx.mask_input(odos, secrets)
+        om, omf = F.mask_input(secrets, odos)
+        assert mf == omf and np.array_equal(m, om), i

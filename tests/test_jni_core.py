@@ -398,3 +398,34 @@ def test_service_party_session_three_parties(J, jctx, F):
         assert e.exception() == (IAE, "the party session is already finished") and e.clean()
         J.mock_clear()
         e.call(SERVICE + "partyFree", None, h)
+
+
+def test_mask_word_makes_no_launch(J):
+    """the per-word maskInput (SecretShareUtil.java:65-68,
+    called once per word from DefaultAmphoraClient.java:155-160's parallel
+    stream) goes through maskWord: two 16-byte region copies in, host
+    arithmetic, one array out -- no critical region, no kernel launch (the
+    context's launch counter stays 0), and toGfp((s - m) mod p) exactly.
+    Needs no GPU: nothing here touches the device."""
+    import random
+    import amphora_amd as A
+    e = Env(J)
+    h = e.call(CLIENT + "ctxCreate", C.c_int64, e.bytes(le16(P)), e.bytes(le16(R)), e.bytes(le16(RINV)), None)
+    assert h != 0 and e.exception() is None
+    rnd = random.Random(11)
+    cases = [(0, 0), (5, 7), (P - 1, 1), (1, P - 1), (P - 1, P - 1)] + \
+            [(rnd.randrange(P), rnd.randrange(P)) for _ in range(200)]
+    for s, m in cases:
+        J.mock_clear()
+        out = e.call(CLIENT + "maskWord", C.c_void_p, C.c_int64(h), e.bytes(le16(s)), e.bytes(le16(m)))
+        assert e.exception() is None and e.clean()
+        assert e.read(out) == le16((s - m) % P * R % P), (s, m)
+        assert J.mock_pins() == 0  # region copies only
+    stats = A._lib._AmphStats()
+    assert A._lib.lib.amph_ctx_stats(C.c_void_p(h), C.byref(stats)) == 0
+    assert stats.kernel_launches == 0
+    # wrong word sizes are refused before the ABI
+    J.mock_clear()
+    assert e.call(CLIENT + "maskWord", C.c_void_p, C.c_int64(h), e.bytes(b"\1" * 8), e.bytes(le16(1))) is None
+    assert e.exception() == (IAE, "maskWord takes two 16-byte words") and e.clean()
+    Env(J).call(CLIENT + "ctxDestroy", None, C.c_int64(h))

@@ -350,3 +350,98 @@ def test_session_partner_fuzz_matches_pair_decode(ctx, F):
             rejected += 1
         s.close()
     assert accepted > 5 and rejected > 5
+
+
+def test_session_device_mode_rejected_text_poisons_and_resubmits(ctx, F):
+    """A device-mode partner text whose verdict word reports a failure: a
+    finish that runs anyway writes poisoned fields ("!!!!" first, no base64
+    decoder accepts them); after amph_party_reset_partner the slot takes a
+    good text and the fields equal the oracle's (the slot was
+    marked filled before the verdict was known)."""
+    import torch
+    n, W = 2, 3000
+    shares, masks, triples = party_inputs(F, n, W)
+    pre = [F.odo_pre(shares[j], 32, masks[j], triples[j]) for j in range(n)]
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    t1 = ctx.party_begin(shares[1], 32, masks[1], triples[1], n).text()
+    at = t1.index(b":") + 3
+    bad_text = dev(np.frombuffer(t1[:at] + b"x" + t1[at + 1:], np.uint8).copy())
+    good_text = dev(np.frombuffer(t1, np.uint8).copy())
+    # finish after a rejected text: poisoned output
+    s = ctx.party_begin_dev(dev(shares[0]), 32, dev(masks[0]), dev(triples[0]), n)
+    bad = s.partner(1, bad_text)
+    fields = s.finish_b64(True)
+    torch.cuda.synchronize()
+    assert int(bad.item()) != 0x7F7F7F7F7F7F7F7F
+    for f in fields:
+        assert f[:4].cpu().numpy().tobytes() == b"!!!!"
+    s.close()
+    # reject, reset the slot, resubmit: exact output
+    s = ctx.party_begin_dev(dev(shares[0]), 32, dev(masks[0]), dev(triples[0]), n)
+    bad = s.partner(1, bad_text)
+    torch.cuda.synchronize()
+    assert int(bad.item()) != 0x7F7F7F7F7F7F7F7F
+    s.reset_partner(1)
+    bad = s.partner(1, good_text)
+    fields = s.finish_b64(True)
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 0x7F7F7F7F7F7F7F7F
+    opened = F.recombine_diffs([pre[0][3], pre[1][3]], [pre[0][4], pre[1][4]])
+    ow, ou = F.odo_post(opened, triples[0], True)
+    want = [base64.b64encode(x.tobytes()) for x in (pre[0][0], pre[0][1], pre[0][2], ow, ou)]
+    assert [f.cpu().numpy().tobytes() for f in fields] == want
+    s.close()
+
+
+def test_session_pool_reclaimed_on_out_of_memory(F):
+    """the party-session buffers the context pools after
+    amph_party_free must not cause an out-of-memory error.  Sessions of
+    growing sizes fill the pool; the GPU is then filled so that the next,
+    larger session fits only if the pooled buffers are freed first -- it
+    must begin, with the pool emptied.  Also: the pool never exceeds
+    AMPH_PARTY_POOL_BYTES (here the 32 GiB default is not reached)."""
+    import torch
+    import amphora_amd as A
+    c = A.Context(P, R, RINV)
+    n = 2
+
+    def dev_inputs(W, seed):
+        sh = c.synth_words(seed=seed, count=2 * W).view(W, 32)
+        mk = c.synth_words(seed=seed + 1, count=4 * W).view(2 * W, 32)
+        tr = c.synth_words(seed=seed + 2, count=12 * W).view(2 * W, 96)
+        return sh, mk, tr
+
+    sizes = [1 << 18, 1 << 19, 1 << 20]
+    for i, W in enumerate(sizes):
+        sh, mk, tr = dev_inputs(W, 10 * i)
+        s = c.party_begin_dev(sh, 32, mk, tr, n)
+        torch.cuda.synchronize()
+        s.close()
+        del sh, mk, tr
+    st = c.stats()
+    assert st["pool_buffers"] >= len(sizes) and st["pool_bytes"] > 0
+    pooled = st["pool_bytes"]
+    big = 1 << 21
+    sh, mk, tr = dev_inputs(big, 99)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    # the big session's buffer ~ 2x the 1 Mi-word session's, the largest pooled
+    need = 2 * max_pooled_estimate(pooled, sizes)
+    free, _ = torch.cuda.mem_get_info()
+    leave = need - pooled // 3  # < need, but need <= leave + pooled
+    filler = torch.empty(max(0, free - leave), dtype=torch.uint8, device="cuda")
+    try:
+        s = c.party_begin_dev(sh, 32, mk, tr, n)
+        torch.cuda.synchronize()
+        st2 = c.stats()
+        s.close()
+    finally:
+        del filler
+        torch.cuda.empty_cache()
+    assert st2["pool_buffers"] == 0, st2
+
+
+def max_pooled_estimate(pooled, sizes):
+    """Bytes of the largest pooled session buffer: sizes double, so it is
+    W_max / sum(W) of the pooled bytes."""
+    return pooled * sizes[-1] // sum(sizes)
