@@ -245,11 +245,37 @@ amph::LaunchCfg cfg(amph_ctx* c, hipStream_t s, size_t words) {
 struct HostIn {
   const uint8_t* host;
   size_t bytes_per_word;
+  size_t base = 0;                        // words into the array where this call starts
+  const amph_host_array* io = nullptr;    // AMPH_F_HOST_IO: the callbacks (host unused)
 };
 struct HostOut {
   uint8_t* host;
   size_t bytes_per_word;
+  size_t base = 0;
+  const amph_host_array* io = nullptr;
 };
+
+// AMPH_F_HOST_IO for the calling thread's current ABI call: set by the entry
+// point (HostIoScope), turned into HostIn/HostOut::io by run_batched before
+// any work leaves this thread.
+thread_local bool g_host_io = false;
+struct HostIoScope {
+  explicit HostIoScope(uint32_t flags) { g_host_io = (flags & AMPH_F_HOST_IO) != 0; }
+  ~HostIoScope() { g_host_io = false; }
+};
+
+// the staging copy of `words` words from word `word` of input x into dst
+amph::CopyTask copy_in(const HostIn& x, size_t word, size_t words, void* dst) {
+  const size_t off = (x.base + word) * x.bytes_per_word, bytes = words * x.bytes_per_word;
+  if (x.io) return amph::CopyTask{dst, nullptr, bytes, x.io, off, false};
+  return amph::CopyTask{dst, x.host + off, bytes};
+}
+amph::CopyTask copy_out(const HostOut& x, size_t word, size_t words, const void* src) {
+  const size_t off = (x.base + word) * x.bytes_per_word, bytes = words * x.bytes_per_word;
+  if (x.io) return amph::CopyTask{nullptr, src, bytes, x.io, off, true};
+  return amph::CopyTask{x.host + off, src, bytes};
+}
+int io_failed() { return fail(AMPH_E_PARAM, "a host array callback (AMPH_F_HOST_IO) failed"); }
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -360,12 +386,12 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
   std::vector<char> in_pinned(ins.size()), out_pinned(outs.size());
   size_t dev_bytes = 0, hin_bytes = 0, hout_bytes = 0;
   for (size_t k = 0; k < ins.size(); ++k) {
-    in_pinned[k] = amph::is_pinned_host(ins[k].host);
+    in_pinned[k] = !ins[k].io && amph::is_pinned_host(ins[k].host);
     dev_bytes += align256(bw * ins[k].bytes_per_word);
     if (!in_pinned[k]) hin_bytes += align256(bw * ins[k].bytes_per_word);
   }
   for (size_t k = 0; k < outs.size(); ++k) {
-    out_pinned[k] = amph::is_pinned_host(outs[k].host);
+    out_pinned[k] = !outs[k].io && amph::is_pinned_host(outs[k].host);
     dev_bytes += align256(bw * outs[k].bytes_per_word);
     if (!out_pinned[k]) hout_bytes += align256(bw * outs[k].bytes_per_word);
   }
@@ -388,13 +414,12 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
     size_t off = 0;
     for (size_t k = 0; k < outs.size(); ++k) {
       if (out_pinned[k]) continue;
-      tasks.push_back({outs[k].host + sl.base * outs[k].bytes_per_word, (char*)sl.hout.p + off,
-                       sl.cnt * outs[k].bytes_per_word});
+      tasks.push_back(copy_out(outs[k], sl.base, sl.cnt, (char*)sl.hout.p + off));
       off += align256(bw * outs[k].bytes_per_word);
     }
-    c->pool->copy(tasks);
+    const int cst = c->pool->copy(tasks);
     sl.busy = false;
-    return AMPH_OK;
+    return cst ? io_failed() : AMPH_OK;
   };
   for (size_t b = 0; b < nb; ++b) {
     amph_ctx::Slot& sl = c->slots[b % S];
@@ -405,19 +430,18 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
     std::vector<const void*> src(ins.size());
     size_t hoff = 0;
     for (size_t k = 0; k < ins.size(); ++k) {
-      const uint8_t* u = ins[k].host + base * ins[k].bytes_per_word;
       if (in_pinned[k]) {
-        src[k] = u;
+        src[k] = ins[k].host + (ins[k].base + base) * ins[k].bytes_per_word;
       } else {
         void* d = (char*)sl.hin.p + hoff;
-        tasks.push_back({d, u, cnt * ins[k].bytes_per_word});
+        tasks.push_back(copy_in(ins[k], base, cnt, d));
         src[k] = d;
         hoff += align256(bw * ins[k].bytes_per_word);
       }
     }
     if (!tasks.empty()) {
       if (sl.used) HIP_TRY(hipEventSynchronize(sl.in_done));
-      c->pool->copy(tasks);
+      if (c->pool->copy(tasks)) return io_failed();
     }
     uint8_t* cur = (uint8_t*)sl.dev.p;
     std::vector<const uint4*> din;
@@ -444,7 +468,7 @@ int run_batched_impl(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
     HIP_TRY(hipStreamWaitEvent(s_out, sl.k_done, 0));
     size_t ooff = 0;
     for (size_t k = 0; k < outs.size(); ++k) {
-      void* dst = outs[k].host + base * outs[k].bytes_per_word;
+      void* dst = outs[k].host + (outs[k].base + base) * outs[k].bytes_per_word;
       if (!out_pinned[k]) {
         dst = (char*)sl.hout.p + ooff;
         ooff += align256(bw * outs[k].bytes_per_word);
@@ -562,7 +586,7 @@ int run_small(amph_ctx* c, size_t words, const std::vector<HostIn>& ins, const s
   std::vector<uint4*> dout;
   for (const HostIn& x : ins) {
     uint8_t* p = a.take(words * x.bytes_per_word);
-    std::memcpy(p, x.host, words * x.bytes_per_word);
+    if (amph::run_copy(copy_in(x, 0, words, p))) return io_failed();
     din.push_back((const uint4*)p);
   }
   for (const HostOut& x : outs) dout.push_back((uint4*)a.take(words * x.bytes_per_word));
@@ -570,7 +594,7 @@ int run_small(amph_ctx* c, size_t words, const std::vector<HostIn>& ins, const s
   if (e != hipSuccess) return small_launch_failed(c, s, e, "kernel launch");
   if (int st = small_end(c, s, with_ff ? 1 : 0)) return st;
   for (size_t k = 0; k < outs.size(); ++k)
-    std::memcpy(outs[k].host, dout[k], words * outs[k].bytes_per_word);
+    if (amph::run_copy(copy_out(outs[k], 0, words, dout[k]))) return io_failed();
   const unsigned long long v = *(volatile unsigned long long*)c->small.p;
   if (with_ff && v != amph::kNoFail) {
     if (first_fail) *first_fail = (int64_t)v;
@@ -593,6 +617,22 @@ template <class Launch>
 int run_batched(amph_ctx* c, size_t words, const std::vector<HostIn>& ins,
                 const std::vector<HostOut>& outs, bool with_ff, int64_t* first_fail,
                 Launch&& launch, size_t ff_scale = 1) {
+  if (g_host_io) {  // the entry point's AMPH_F_HOST_IO: the pointers are descriptors
+    std::vector<HostIn> ins2(ins);
+    std::vector<HostOut> outs2(outs);
+    for (HostIn& x : ins2) {
+      x.io = (const amph_host_array*)x.host;
+      if (words && (!x.io || !x.io->read)) return fail(AMPH_E_PARAM, "host array without a read callback");
+    }
+    for (HostOut& x : outs2) {
+      x.io = (const amph_host_array*)x.host;
+      if (words && (!x.io || !x.io->write)) return fail(AMPH_E_PARAM, "host array without a write callback");
+    }
+    g_host_io = false;  // consumed: the nested call sees explicit descriptors
+    const int st = run_batched(c, words, ins2, outs2, with_ff, first_fail, launch, ff_scale);
+    g_host_io = true;
+    return st;
+  }
   if (!c->sub.empty()) return run_sharded(c, words, ins, outs, with_ff, first_fail, launch, ff_scale);
   const size_t bytes = call_bytes(words, ins, outs);
   if (small_call(c, bytes)) return run_small(c, words, ins, outs, with_ff, first_fail, launch, bytes);
@@ -629,9 +669,9 @@ int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
   for (size_t d = 0; d < used; ++d) {
     const size_t start = d * per, cnt = std::min(per, words - start);
     std::vector<HostIn> in2(ins);
-    for (auto& x : in2) x.host += start * x.bytes_per_word;
+    for (auto& x : in2) x.base += start;
     std::vector<HostOut> out2(outs);
-    for (auto& x : out2) x.host += start * x.bytes_per_word;
+    for (auto& x : out2) x.base += start;
     amph_ctx* s = g->sub[d];
     s->worker->post([&, d, s, cnt, in2 = std::move(in2), out2 = std::move(out2)]() {
       try {
@@ -657,6 +697,14 @@ int run_sharded(amph_ctx* g, size_t words, const std::vector<HostIn>& ins,
 }
 
 int check_ctx(amph_ctx* c) { return c ? AMPH_OK : fail(AMPH_E_PARAM, "null context"); }
+
+// Entry of a call that accepts AMPH_F_HOST_IO / one that refuses it.
+#define AMPH_HOST_IO_ENTRY(flags)                                                      \
+  if (((flags) & AMPH_F_HOST_IO) && ((flags) & AMPH_F_DEVICE))                         \
+    return fail(AMPH_E_PARAM, "AMPH_F_HOST_IO and AMPH_F_DEVICE exclude each other");  \
+  HostIoScope host_io_scope_(flags)
+#define AMPH_NO_HOST_IO(flags) \
+  if ((flags) & AMPH_F_HOST_IO) return fail(AMPH_E_PARAM, "AMPH_F_HOST_IO is not accepted by this call")
 
 int odo_words(const amph_odo* odos, int n, size_t* words) {
   if (!odos || n < 1 || n > AMPH_MAX_PARTIES)
@@ -891,6 +939,7 @@ int amph_ctx_set_batch_words(amph_ctx* c, size_t words) {
 int amph_recombine_verify(amph_ctx* c, const amph_odo* odos, int n, uint8_t* out_secrets,
                           int64_t* first_fail, uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
   size_t W;
   if (int st = odo_words(odos, n, &W)) return st;
   if (W && !out_secrets) return fail(AMPH_E_PARAM, "null output");
@@ -925,6 +974,7 @@ int amph_mask_input(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* sec
                     size_t n_secrets, uint8_t* out_masked, int64_t* first_fail, uint32_t flags,
                     void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
   size_t W;
   if (int st = odo_words(odos, n, &W)) return st;
   if (n_secrets > W)
@@ -963,7 +1013,7 @@ int amph_mask_input(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* sec
   // i < secret.size() only, but verifyOutputDeliveryObjects checked them all)
   std::vector<HostIn> tins;
   for (int k = 0; k < 5; ++k)
-    for (int j = 0; j < n; ++j) tins.push_back({odo_field(odos[j], k) + n_secrets * 16, 16});
+    for (int j = 0; j < n; ++j) tins.push_back({odo_field(odos[j], k), 16, n_secrets});
   int64_t tf = -1;
   st = run_batched(c, W - n_secrets, tins, {}, true, &tf,
                    [&](auto& din, auto&, size_t cnt, unsigned long long* ff,
@@ -980,6 +1030,7 @@ int amph_mask_input(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* sec
 int amph_recombine(amph_ctx* c, const uint8_t* const* shares, int n, size_t nbytes, uint8_t* out,
                    uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
   if (!shares || n < 1 || n > AMPH_MAX_PARTIES) return fail(AMPH_E_PARAM, "n_parties must be in [1, 16]");
   const size_t W = nbytes / AMPH_WORD_WIDTH;
   if (W && !out) return fail(AMPH_E_PARAM, "null output");
@@ -1011,6 +1062,7 @@ int amph_verify(amph_ctx* c, const uint8_t* y, const uint8_t* r, const uint8_t* 
                 const uint8_t* v, const uint8_t* w, size_t words, int64_t* first_fail,
                 uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
   if (words && (!y || !r || !u || !v || !w)) return fail(AMPH_E_PARAM, "null input");
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({y, r, u, v, w})) return st;
@@ -1054,6 +1106,7 @@ int amph_convert_share(amph_ctx* c, const uint8_t* masked, const uint8_t* tuples
                        const uint8_t mac_key_le[16], int use_zero, uint8_t* out, uint32_t flags,
                        void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
   if (!mac_key_le) return fail(AMPH_E_PARAM, "null mac key");
   if (words && (!masked || !tuples || !out)) return fail(AMPH_E_PARAM, "null buffer");
   // [alpha] = alpha R mod p, computed once per call on the host
@@ -1080,6 +1133,7 @@ int amph_odo_pre(amph_ctx* c, const uint8_t* share_data, size_t share_stride,
                  uint8_t* orr, uint8_t* ov, uint8_t* omag, uint8_t* oneg, uint32_t flags,
                  void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
   if (share_stride != 16 && share_stride != 32)
     return fail(AMPH_E_PARAM, "share_stride must be 16 or 32");
   if (words && (!share_data || !masks || !triples || !oy || !orr || !ov || !omag || !oneg))
@@ -1108,6 +1162,7 @@ int amph_odo_pre(amph_ctx* c, const uint8_t* share_data, size_t share_stride,
 int amph_open_diffs(amph_ctx* c, const uint8_t* const* mags, const uint8_t* const* negs, int n,
                     size_t n_pairs, uint8_t* out, uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
   if (!mags || !negs || n < 1 || n > AMPH_MAX_PARTIES) return fail(AMPH_E_PARAM, "n_parties must be in [1, 16]");
   if (n_pairs % 2) return fail(AMPH_E_LEN, "n_pairs must be 2 * words");
   const size_t W = n_pairs / 2;
@@ -1146,6 +1201,7 @@ int amph_open_diffs(amph_ctx* c, const uint8_t* const* mags, const uint8_t* cons
 int amph_odo_post(amph_ctx* c, const uint8_t* opened, const uint8_t* triples, size_t words,
                   int is_player0, uint8_t* ow, uint8_t* ou, uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
   if (words && (!opened || !triples || !ow || !ou)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({opened, triples, ow, ou})) return st;
@@ -1169,6 +1225,7 @@ int amph_open_post(amph_ctx* c, const uint8_t* const* mags, const uint8_t* const
                    const uint8_t* triples, size_t words, int is_player0, uint8_t* ow, uint8_t* ou,
                    uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
   if (!mags || !negs || n < 1 || n > AMPH_MAX_PARTIES) return fail(AMPH_E_PARAM, "n_parties must be in [1, 16]");
   if (words && (!triples || !ow || !ou)) return fail(AMPH_E_PARAM, "null buffer");
   for (int j = 0; j < n; ++j)
@@ -1208,6 +1265,7 @@ int amph_open_post(amph_ctx* c, const uint8_t* const* mags, const uint8_t* const
 int amph_to_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, uint32_t flags,
                 void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
   if (words && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({in, out})) return st;
@@ -1226,6 +1284,7 @@ int amph_to_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, uint
 int amph_from_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, uint32_t flags,
                   void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
   if (words && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({in, out})) return st;
@@ -1244,6 +1303,7 @@ int amph_from_gfp(amph_ctx* c, const uint8_t* in, size_t words, uint8_t* out, ui
 int amph_mask_words(amph_ctx* c, const uint8_t* secrets, const uint8_t* masks, size_t words,
                     uint8_t* out, uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
   if (words && (!secrets || !masks || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({secrets, masks, out})) return st;
@@ -1304,6 +1364,7 @@ extern "C" {
 int amph_base64_encode(amph_ctx* c, const uint8_t* in, size_t nbytes, char* out, uint32_t flags,
                        void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_NO_HOST_IO(flags);
   if (nbytes && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     HIP_TRY(use_device(c->device));
@@ -1328,6 +1389,7 @@ int amph_base64_encode(amph_ctx* c, const uint8_t* in, size_t nbytes, char* out,
 int amph_base64_decode(amph_ctx* c, const char* in, size_t nchars, uint8_t* out,
                        size_t* out_bytes, int64_t* bad_index, uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_NO_HOST_IO(flags);
   if (nchars % 4) return fail(AMPH_E_LEN, "base64 input length must be a multiple of 4");
   if (nchars && (!in || !out)) return fail(AMPH_E_PARAM, "null buffer");
   if (bad_index && !(flags & AMPH_F_DEVICE)) *bad_index = -1;
@@ -1384,6 +1446,7 @@ int amph_base64_decode(amph_ctx* c, const char* in, size_t nchars, uint8_t* out,
 int amph_base64_encode_words(amph_ctx* c, const uint8_t* words16, size_t words, char* out24,
                              uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_NO_HOST_IO(flags);
   if (words && (!words16 || !out24)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({words16})) return st;
@@ -1403,6 +1466,7 @@ int amph_base64_encode_words(amph_ctx* c, const uint8_t* words16, size_t words, 
 int amph_base64_decode_words(amph_ctx* c, const char* in24, size_t words, uint8_t* out16,
                              int64_t* bad_index, uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_NO_HOST_IO(flags);
   if (words && (!in24 || !out16)) return fail(AMPH_E_PARAM, "null buffer");
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_words({out16})) return st;
@@ -1484,6 +1548,7 @@ int amph_exchange_encode(amph_ctx* c, const uint8_t* mag16, const uint8_t* neg, 
                          char* out, size_t out_cap, uint64_t* out_len, uint32_t flags,
                          void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_NO_HOST_IO(flags);
   if (!out || !out_len || (npairs && (!mag16 || !neg))) return fail(AMPH_E_PARAM, "null buffer");
   HIP_TRY(use_device(c->device));
   const size_t maxb = amph::xenc_max_bytes(npairs);
@@ -1554,6 +1619,7 @@ int amph_exchange_encode(amph_ctx* c, const uint8_t* mag16, const uint8_t* neg, 
 int amph_exchange_decode(amph_ctx* c, const char* text, size_t len, size_t npairs, uint8_t* mag16,
                          uint8_t* neg, int64_t* bad_index, uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_NO_HOST_IO(flags);
   if ((len && !text) || (npairs && (!mag16 || !neg))) return fail(AMPH_E_PARAM, "null buffer");
   HIP_TRY(use_device(c->device));
   if (flags & AMPH_F_DEVICE) {
@@ -1741,6 +1807,7 @@ int amph_recombine_verify_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size
                               uint8_t* out_secrets, int64_t* first_fail, int64_t* bad_char,
                               uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_NO_HOST_IO(flags);
   size_t nchars;
   uint32_t pad;
   if (int st = wire_check(odos, n, words, &nchars, &pad)) return st;
@@ -1791,6 +1858,7 @@ int amph_mask_input_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size_t wor
                         const uint8_t* secrets, size_t n_secrets, uint8_t* out16, char* out24,
                         int64_t* first_fail, int64_t* bad_char, uint32_t flags, void* stream) {
   if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_NO_HOST_IO(flags);
   size_t nchars;
   uint32_t pad;
   if (int st = wire_check(odos, n, words, &nchars, &pad)) return st;

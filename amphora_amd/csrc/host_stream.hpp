@@ -20,6 +20,8 @@
 #include <thread>
 #include <vector>
 
+#include "../../include/amphora.h"
+
 namespace amph {
 
 struct PinnedBuf {
@@ -45,14 +47,29 @@ struct PinnedBuf {
   }
 };
 
+// One staging copy: memcpy(dst, src, bytes), or -- for an AMPH_F_HOST_IO
+// array -- its read (io_write false: array[io_off ..] -> dst) or write
+// (io_write true: src -> array[io_off ..]) callback.
 struct CopyTask {
   void* dst;
   const void* src;
   size_t bytes;
+  const amph_host_array* io = nullptr;
+  size_t io_off = 0;
+  bool io_write = false;
 };
 
+inline int run_copy(const CopyTask& c) {
+  if (!c.io) {
+    std::memcpy(c.dst, c.src, c.bytes);
+    return 0;
+  }
+  return c.io_write ? c.io->write(c.io, c.io_off, c.bytes, c.src) : c.io->read(c.io, c.io_off, c.bytes, c.dst);
+}
+
 // Persistent pool: copy(tasks) splits every task into chunks of >= 4 MiB and
-// runs them on the workers and the calling thread; returns when all are done.
+// runs them on the workers and the calling thread; returns when all are done,
+// with 0 or the first nonzero callback status (the other chunks still run).
 class CopyPool {
  public:
   explicit CopyPool(int threads) {
@@ -68,17 +85,24 @@ class CopyPool {
   }
   int threads() const { return (int)workers_.size() + 1; }
 
-  void copy(const std::vector<CopyTask>& tasks) {
+  int copy(const std::vector<CopyTask>& tasks) {
     std::vector<CopyTask> chunks;
     const size_t kChunk = (size_t)4 << 20;
     for (const auto& t : tasks)
-      for (size_t off = 0; off < t.bytes; off += kChunk)
-        chunks.push_back({(char*)t.dst + off, (const char*)t.src + off, std::min(kChunk, t.bytes - off)});
-    if (chunks.empty()) return;
+      for (size_t off = 0; off < t.bytes; off += kChunk) {
+        CopyTask c = t;
+        c.dst = (char*)t.dst + off;
+        c.src = (const char*)t.src + off;
+        c.bytes = std::min(kChunk, t.bytes - off);
+        c.io_off = t.io_off + off;
+        chunks.push_back(c);
+      }
+    if (chunks.empty()) return 0;
     std::unique_lock<std::mutex> lk(m_);
     jobs_ = &chunks;
     next_ = 0;
     remaining_ = chunks.size();
+    status_ = 0;
     ++gen_;
     lk.unlock();
     cv_.notify_all();
@@ -86,6 +110,7 @@ class CopyPool {
     lk.lock();
     done_cv_.wait(lk, [&] { return remaining_ == 0; });
     jobs_ = nullptr;
+    return status_;
   }
 
  private:
@@ -97,8 +122,9 @@ class CopyPool {
         if (!jobs_ || next_ >= jobs_->size()) return;
         c = (*jobs_)[next_++];
       }
-      std::memcpy(c.dst, c.src, c.bytes);
+      const int st = run_copy(c);
       std::lock_guard<std::mutex> g(m_);
+      if (st && !status_) status_ = st;
       if (--remaining_ == 0) done_cv_.notify_all();
     }
   }
@@ -121,6 +147,7 @@ class CopyPool {
   size_t next_ = 0;
   size_t remaining_ = 0;
   size_t gen_ = 0;
+  int status_ = 0;
   bool stop_ = false;
 };
 
@@ -150,7 +177,6 @@ class DeviceWorker {
     }
     cv_.notify_one();
   }
-  std::thread::id id() const { return th_.get_id(); }
 
  private:
   void loop() {

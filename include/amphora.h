@@ -88,6 +88,30 @@ extern "C" {
  * The caller sets it to AMPH_NO_FAILURE once before a run of calls (saves
  * one memset launch per call; used by bench.py and for repeated passes). */
 #define AMPH_F_ACCUMULATE 0x2u
+/* Host arrays behind callbacks: every buffer argument of the call is a
+ * `const amph_host_array*` (cast to the argument's pointer type) instead of
+ * host memory, and the library moves the words with the descriptors' read /
+ * write callbacks as its batched pipeline consumes and produces them (a JNI
+ * layer's Get/SetByteArrayRegion: the Java heap is not pinned across the GPU
+ * call -- INTEGRATION.md).  Accepted by the word-array calls that stream
+ * through the host pipeline: amph_recombine_verify, amph_mask_input,
+ * amph_recombine, amph_verify, amph_mask_words, amph_to_gfp, amph_from_gfp,
+ * amph_convert_share, amph_odo_pre, amph_open_diffs, amph_odo_post,
+ * amph_open_post; refused (AMPH_E_PARAM) by every other call with flags, and
+ * exclusive with AMPH_F_DEVICE.  Offsets and sizes are in bytes from the
+ * start of the array the descriptor stands for; a call reads only what its
+ * word count implies, so the caller checks array lengths first. */
+#define AMPH_F_HOST_IO 0x4u
+typedef struct amph_host_array {
+  /* copy `bytes` bytes at byte offset `off` of the array into dst (inputs)
+   * or from src into it (outputs); return 0, or nonzero to fail the call
+   * (AMPH_E_PARAM, after the copies in flight have ended).  Called from the
+   * library's staging threads -- several at once, for disjoint ranges --
+   * and never after the call has returned. */
+  int (*read)(const struct amph_host_array* a, size_t off, size_t bytes, void* dst);
+  int (*write)(const struct amph_host_array* a, size_t off, size_t bytes, const void* src);
+  void* user;
+} amph_host_array;
 
 /* value of a device-side first_fail word when every word verified */
 #define AMPH_NO_FAILURE ((int64_t)0x7F7F7F7F7F7F7F7FLL)

@@ -22,6 +22,17 @@
  * IllegalArgumentException for length / argument errors (the reference's
  * messages where it has one), IllegalStateException for runtime errors.
  *
+ * Large calls: a critical region blocks the
+ * JVM's garbage collector for as long as it is open, and a GPU call at C4
+ * sizes lasts tens of milliseconds.  So only calls that move at most
+ * AMPH_JNI_REGION_BYTES (default 2 MiB, libamphora_hip's small-call size) pin
+ * their arrays.  Above it the word-array calls hand libamphora_hip
+ * amph_host_array descriptors (AMPH_F_HOST_IO): the library's staging threads
+ * copy each batch with Get/SetByteArrayRegion as its pipeline consumes and
+ * produces it (those threads attach to the VM as daemons once), so no
+ * critical region is open during the GPU call; the party-session calls copy
+ * their arrays into native buffers with region copies instead.
+ *
  * Build: jni/Makefile (skipped when no JDK is found -- this image has none).
  */
 #include <jni.h>
@@ -110,6 +121,126 @@ static int pin_all(JNIEnv* env, Pin* pins, int count) {
   return 0;
 }
 
+/* ---- large calls: region copies instead of pins ----------------------------- */
+static size_t region_bytes(void) {
+  const char* e = getenv("AMPH_JNI_REGION_BYTES");
+  return e ? (size_t)strtoull(e, NULL, 10) : (size_t)2 << 20;
+}
+
+static size_t total_len(const Pin* pins, int count) {
+  size_t t = 0;
+  for (int i = 0; i < count; ++i) t += (size_t)pins[i].len;
+  return t;
+}
+
+typedef struct {
+  amph_host_array a; /* first: the descriptor libamphora_hip sees */
+  JavaVM* vm;
+  jbyteArray gref;
+} JArr;
+
+/* the JNIEnv of whichever thread runs the callback: the calling Java thread,
+   or one of libamphora_hip's staging threads, attached as a daemon on first use */
+static JNIEnv* env_here(JavaVM* vm) {
+  JNIEnv* e = NULL;
+  if ((*vm)->GetEnv(vm, (void**)&e, JNI_VERSION_1_6) == JNI_OK) return e;
+  if ((*vm)->AttachCurrentThreadAsDaemon(vm, (void**)&e, NULL) != JNI_OK) return NULL;
+  return e;
+}
+
+static int jarr_read(const amph_host_array* a, size_t off, size_t bytes, void* dst) {
+  const JArr* j = (const JArr*)a;
+  JNIEnv* e = env_here(j->vm);
+  if (!e) return -1;
+  (*e)->GetByteArrayRegion(e, j->gref, (jsize)off, (jsize)bytes, (jbyte*)dst);
+  if ((*e)->ExceptionCheck(e)) {  /* out of range: the lengths were checked, so not expected */
+    (*e)->ExceptionClear(e);
+    return -1;
+  }
+  return 0;
+}
+
+static int jarr_write(const amph_host_array* a, size_t off, size_t bytes, const void* src) {
+  const JArr* j = (const JArr*)a;
+  JNIEnv* e = env_here(j->vm);
+  if (!e) return -1;
+  (*e)->SetByteArrayRegion(e, j->gref, (jsize)off, (jsize)bytes, (const jbyte*)src);
+  if ((*e)->ExceptionCheck(e)) {
+    (*e)->ExceptionClear(e);
+    return -1;
+  }
+  return 0;
+}
+
+typedef struct {
+  int regions;
+  JArr ja[5 * MAXP + 2];
+} Access;
+
+static void release_access(JNIEnv* env, Pin* pins, int count, int first_output, Access* acc);
+
+/* Small call: pin every array.  Large call: a global reference and an
+   amph_host_array descriptor per array (pins[i].p points at it), and the
+   core passes AMPH_F_HOST_IO.  -1: an exception is pending, nothing held. */
+static int acquire(JNIEnv* env, Pin* pins, int count, Access* acc) {
+  acc->regions = total_len(pins, count) > region_bytes();
+  if (!acc->regions) return pin_all(env, pins, count);
+  JavaVM* vm = NULL;
+  if ((*env)->GetJavaVM(env, &vm) != 0 || !vm) return throw_arg(env, "no JavaVM");
+  for (int i = 0; i < count; ++i) {
+    acc->ja[i].gref = (jbyteArray)(*env)->NewGlobalRef(env, pins[i].ref);
+    if (!acc->ja[i].gref) { /* OutOfMemoryError pending */
+      release_access(env, pins, i, i, acc);
+      return -1;
+    }
+    acc->ja[i].a.read = jarr_read;
+    acc->ja[i].a.write = jarr_write;
+    acc->ja[i].a.user = NULL;
+    acc->ja[i].vm = vm;
+    pins[i].p = (jbyte*)&acc->ja[i].a;
+  }
+  amphj_set_host_io(1);
+  return 0;
+}
+
+static void release_access(JNIEnv* env, Pin* pins, int count, int first_output, Access* acc) {
+  if (!acc->regions) {
+    unpin_all(env, pins, count, first_output);
+    return;
+  }
+  amphj_set_host_io(0);
+  for (int i = 0; i < count; ++i) {
+    (*env)->DeleteGlobalRef(env, acc->ja[i].gref);
+    pins[i].p = NULL;
+  }
+}
+
+/* party-session calls above the threshold: native copies, filled / drained
+   with region copies, so nothing is pinned while the session runs */
+static int stage_native(JNIEnv* env, Pin* pins, int count, int first_output) {
+  for (int i = 0; i < count; ++i) {
+    if (!pins[i].ref) continue;
+    pins[i].p = (jbyte*)malloc(pins[i].len ? (size_t)pins[i].len : 1);
+    if (!pins[i].p) {
+      for (int k = 0; k < i; ++k) free(pins[k].p), pins[k].p = NULL;
+      jclass c = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+      if (c) (*env)->ThrowNew(env, c, "native staging of a Java array");
+      return -1;
+    }
+    if (i < first_output) (*env)->GetByteArrayRegion(env, pins[i].ref, 0, pins[i].len, pins[i].p);
+  }
+  return 0;
+}
+
+static void unstage_native(JNIEnv* env, Pin* pins, int count, int first_output, int commit) {
+  for (int i = 0; i < count; ++i) {
+    if (!pins[i].ref || !pins[i].p) continue;
+    if (commit && i >= first_output) (*env)->SetByteArrayRegion(env, pins[i].ref, 0, pins[i].len, pins[i].p);
+    free(pins[i].p);
+    pins[i].p = NULL;
+  }
+}
+
 static void ptrs_of(const Pin* pins, int count, const uint8_t** ptrs, size_t* lens) {
   for (int i = 0; i < count; ++i) {
     ptrs[i] = (const uint8_t*)pins[i].p;
@@ -171,11 +302,12 @@ JNIEXPORT jlong JNICALL CLIENT(recombineVerify)(JNIEnv* env, jclass cls, jlong c
   const uint8_t* ptrs[5 * MAXP];
   size_t lens[5 * MAXP];
   int64_t fail = -1;
-  if (pin_all(env, pins, 5 * n + 1)) return -1;
+  Access acc;
+  if (acquire(env, pins, 5 * n + 1, &acc)) return -1;
   ptrs_of(pins, 5 * n, ptrs, lens);
   const int st = amphj_recombine_verify(CTX(ctx), n, ptrs, lens, (uint8_t*)pins[5 * n].p,
                                         (size_t)pins[5 * n].len, &fail);
-  unpin_all(env, pins, 5 * n + 1, 5 * n);
+  release_access(env, pins, 5 * n + 1, 5 * n, &acc);
   if (st != AMPH_OK && st != AMPH_E_VERIFY) throw_status(env, st);
   return st == AMPH_E_VERIFY ? (jlong)fail : -1;
 }
@@ -192,11 +324,12 @@ JNIEXPORT jlong JNICALL CLIENT(maskInput)(JNIEnv* env, jclass cls, jlong ctx, jo
   const uint8_t* ptrs[5 * MAXP];
   size_t lens[5 * MAXP];
   int64_t fail = -1;
-  if (pin_all(env, pins, 5 * n + 2)) return -1;
+  Access acc;
+  if (acquire(env, pins, 5 * n + 2, &acc)) return -1;
   ptrs_of(pins, 5 * n, ptrs, lens);
   const int st = amphj_mask_input(CTX(ctx), n, ptrs, lens, (const uint8_t*)pins[5 * n].p, (size_t)pins[5 * n].len,
                                   (uint8_t*)pins[5 * n + 1].p, (size_t)pins[5 * n + 1].len, &fail);
-  unpin_all(env, pins, 5 * n + 2, 5 * n + 1);
+  release_access(env, pins, 5 * n + 2, 5 * n + 1, &acc);
   if (st != AMPH_OK && st != AMPH_E_VERIFY) throw_status(env, st);
   return st == AMPH_E_VERIFY ? (jlong)fail : -1;
 }
@@ -209,10 +342,11 @@ JNIEXPORT void JNICALL CLIENT(recombine)(JNIEnv* env, jclass cls, jlong ctx, job
   if (refs_list(env, shares, pins, &n) || ref(env, out, &pins[n])) return;
   const uint8_t* ptrs[MAXP];
   size_t lens[MAXP];
-  if (pin_all(env, pins, n + 1)) return;
+  Access acc;
+  if (acquire(env, pins, n + 1, &acc)) return;
   ptrs_of(pins, n, ptrs, lens);
   const int st = amphj_recombine(CTX(ctx), n, ptrs, lens, (uint8_t*)pins[n].p, (size_t)pins[n].len);
-  unpin_all(env, pins, n + 1, n);
+  release_access(env, pins, n + 1, n, &acc);
   if (st != AMPH_OK) throw_status(env, st);
 }
 
@@ -227,10 +361,11 @@ JNIEXPORT jlong JNICALL CLIENT(verify)(JNIEnv* env, jclass cls, jlong ctx, jbyte
   const uint8_t* ptrs[5];
   size_t lens[5];
   int64_t fail = -1;
-  if (pin_all(env, pins, 5)) return -1;
+  Access acc;
+  if (acquire(env, pins, 5, &acc)) return -1;
   ptrs_of(pins, 5, ptrs, lens);
   const int st = amphj_verify(CTX(ctx), ptrs, lens, &fail);
-  unpin_all(env, pins, 5, 5);
+  release_access(env, pins, 5, 5, &acc);
   if (st != AMPH_OK && st != AMPH_E_VERIFY) throw_status(env, st);
   return st == AMPH_E_VERIFY ? (jlong)fail : -1;
 }
@@ -241,11 +376,12 @@ JNIEXPORT void JNICALL CLIENT(maskWords)(JNIEnv* env, jclass cls, jlong ctx, jby
   (void)cls;
   Pin pins[3];
   if (ref(env, secrets, &pins[0]) || ref(env, masks, &pins[1]) || ref(env, out, &pins[2])) return;
-  if (pin_all(env, pins, 3)) return;
+  Access acc;
+  if (acquire(env, pins, 3, &acc)) return;
   const int st = amphj_mask_words(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len,
                                   (const uint8_t*)pins[1].p, (size_t)pins[1].len, (uint8_t*)pins[2].p,
                                   (size_t)pins[2].len);
-  unpin_all(env, pins, 3, 2);
+  release_access(env, pins, 3, 2, &acc);
   if (st != AMPH_OK) throw_status(env, st);
 }
 
@@ -357,16 +493,19 @@ JNIEXPORT void JNICALL SERVICE(convertShare)(JNIEnv* env, jclass cls, jlong ctx,
                                              jbyteArray tuples, jbyteArray macKeyLe, jboolean useZeroInputAsData,
                                              jbyteArray out) {
   (void)cls;
-  Pin pins[4];
-  if (ref(env, masked, &pins[0]) || ref(env, tuples, &pins[1]) || ref(env, macKeyLe, &pins[2]) ||
-      ref(env, out, &pins[3]))
+  Pin pins[3], key;
+  if (ref(env, masked, &pins[0]) || ref(env, tuples, &pins[1]) || ref(env, out, &pins[2]) ||
+      ref(env, macKeyLe, &key))
     return;
-  if (pin_all(env, pins, 4)) return;
+  jbyte k16[16] = {0};  /* the key is read on this thread: a region copy, never a descriptor */
+  if (key.len == 16) (*env)->GetByteArrayRegion(env, macKeyLe, 0, 16, k16);
+  Access acc;
+  if (acquire(env, pins, 3, &acc)) return;
   const int st = amphj_convert_share(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len,
-                                     (const uint8_t*)pins[1].p, (size_t)pins[1].len, (const uint8_t*)pins[2].p,
-                                     (size_t)pins[2].len, useZeroInputAsData ? 1 : 0, (uint8_t*)pins[3].p,
-                                     (size_t)pins[3].len);
-  unpin_all(env, pins, 4, 3);
+                                     (const uint8_t*)pins[1].p, (size_t)pins[1].len, (const uint8_t*)k16,
+                                     (size_t)key.len, useZeroInputAsData ? 1 : 0, (uint8_t*)pins[2].p,
+                                     (size_t)pins[2].len);
+  release_access(env, pins, 3, 2, &acc);
   if (st != AMPH_OK) throw_status(env, st);
 }
 
@@ -383,13 +522,14 @@ JNIEXPORT void JNICALL SERVICE(odoPre)(JNIEnv* env, jclass cls, jlong ctx, jbyte
     throw_arg(env, "The provided shares must be of the same length");
     return;
   }
-  if (pin_all(env, pins, 8)) return;
+  Access acc;
+  if (acquire(env, pins, 8, &acc)) return;
   const int st = amphj_odo_pre(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len, stride,
                                (const uint8_t*)pins[1].p, (size_t)pins[1].len, (const uint8_t*)pins[2].p,
                                (size_t)pins[2].len, (uint8_t*)pins[3].p, (uint8_t*)pins[4].p, (uint8_t*)pins[5].p,
                                (size_t)pins[3].len, (uint8_t*)pins[6].p, (size_t)pins[6].len, (uint8_t*)pins[7].p,
                                (size_t)pins[7].len);
-  unpin_all(env, pins, 8, 3);
+  release_access(env, pins, 8, 3, &acc);
   if (st != AMPH_OK) throw_status(env, st);
 }
 
@@ -411,12 +551,13 @@ JNIEXPORT void JNICALL SERVICE(openPost)(JNIEnv* env, jclass cls, jlong ctx, job
   }
   const uint8_t* ptrs[2 * MAXP];
   size_t lens[2 * MAXP];
-  if (pin_all(env, pins, 2 * n + 3)) return;
+  Access acc;
+  if (acquire(env, pins, 2 * n + 3, &acc)) return;
   ptrs_of(pins, 2 * n, ptrs, lens);
   const int st = amphj_open_post(CTX(ctx), n, ptrs, lens, ptrs + n, lens + n, (const uint8_t*)pins[2 * n].p,
                                  (size_t)pins[2 * n].len, isPlayer0 ? 1 : 0, (uint8_t*)pins[2 * n + 1].p,
                                  (uint8_t*)pins[2 * n + 2].p, (size_t)pins[2 * n + 1].len);
-  unpin_all(env, pins, 2 * n + 3, 2 * n + 1);
+  release_access(env, pins, 2 * n + 3, 2 * n + 1, &acc);
   if (st != AMPH_OK) throw_status(env, st);
 }
 
@@ -511,13 +652,15 @@ JNIEXPORT jlong JNICALL SERVICE(partyBegin)(JNIEnv* env, jclass cls, jlong ctx, 
     throw_arg(env, "The provided shares must be of the same length");
     return 0;
   }
-  if (pin_present(env, pins, 6)) return 0;
+  const int staged = total_len(pins, 6) > region_bytes();
+  if (staged ? stage_native(env, pins, 6, 3) : pin_present(env, pins, 6)) return 0;
   void* session = NULL;
   const int st = amphj_party_begin(CTX(ctx), (const uint8_t*)pins[0].p, (size_t)pins[0].len, stride,
                                    (const uint8_t*)pins[1].p, (size_t)pins[1].len, (const uint8_t*)pins[2].p,
                                    (size_t)pins[2].len, nParties, (uint8_t*)pins[3].p, (uint8_t*)pins[4].p,
                                    (uint8_t*)pins[5].p, (size_t)pins[3].len, &session);
-  unpin_all(env, pins, 6, 3);
+  if (staged) unstage_native(env, pins, 6, 3, st == AMPH_OK);
+  else unpin_all(env, pins, 6, 3);
   if (st != AMPH_OK) {
     throw_status(env, st);
     return 0;
@@ -534,9 +677,12 @@ JNIEXPORT jbyteArray JNICALL SERVICE(partyText)(JNIEnv* env, jclass cls, jlong s
   jbyteArray out = (*env)->NewByteArray(env, (jsize)len);
   if (!out) return NULL; /* OutOfMemoryError pending */
   Pin pin;
-  if (ref(env, out, &pin) || pin_all(env, &pin, 1)) return NULL;
+  if (ref(env, out, &pin)) return NULL;
+  const int staged = (size_t)pin.len > region_bytes();
+  if (staged ? stage_native(env, &pin, 1, 0) : pin_all(env, &pin, 1)) return NULL;
   const int st = amphj_party_text(CTX(session), (char*)pin.p, (size_t)pin.len);
-  unpin_all(env, &pin, 1, 0);
+  if (staged) unstage_native(env, &pin, 1, 0, st == AMPH_OK);
+  else unpin_all(env, &pin, 1, 0);
   if (st != AMPH_OK) {
     throw_status(env, st);
     return NULL;
@@ -554,9 +700,26 @@ JNIEXPORT void JNICALL SERVICE(partyPartner)(JNIEnv* env, jclass cls, jlong sess
     throw_arg(env, "interimValues span outside the body");
     return;
   }
-  if (pin_all(env, &pin, 1)) return;
-  const int st = amphj_party_partner(CTX(session), slot, (const char*)pin.p + off, (size_t)len);
-  unpin_all(env, &pin, 1, 1);
+  /* above the threshold only the interimValues span is copied out of the body */
+  const int staged = (size_t)len > region_bytes();
+  Pin span = {pin.ref, len, NULL};
+  const char* text;
+  if (staged) {
+    span.p = (jbyte*)malloc(len ? (size_t)len : 1);
+    if (!span.p) {
+      jclass c = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+      if (c) (*env)->ThrowNew(env, c, "native staging of a Java array");
+      return;
+    }
+    (*env)->GetByteArrayRegion(env, body, off, len, span.p);
+    text = (const char*)span.p;
+  } else {
+    if (pin_all(env, &pin, 1)) return;
+    text = (const char*)pin.p + off;
+  }
+  const int st = amphj_party_partner(CTX(session), slot, text, (size_t)len);
+  if (staged) free(span.p);
+  else unpin_all(env, &pin, 1, 1);
   if (st != AMPH_OK) throw_status(env, st);
 }
 
@@ -570,10 +733,12 @@ JNIEXPORT void JNICALL SERVICE(partyFinish)(JNIEnv* env, jclass cls, jlong sessi
     throw_arg(env, "The provided shares must be of the same length");
     return;
   }
-  if (pin_all(env, pins, 2)) return;
+  const int staged = total_len(pins, 2) > region_bytes();
+  if (staged ? stage_native(env, pins, 2, 0) : pin_all(env, pins, 2)) return;
   const int st = amphj_party_finish(CTX(session), isPlayer0 ? 1 : 0, (uint8_t*)pins[0].p, (uint8_t*)pins[1].p,
                                     (size_t)pins[0].len);
-  unpin_all(env, pins, 2, 0);
+  if (staged) unstage_native(env, pins, 2, 0, st == AMPH_OK);
+  else unpin_all(env, pins, 2, 0);
   if (st != AMPH_OK) throw_status(env, st);
 }
 
@@ -588,7 +753,8 @@ JNIEXPORT void JNICALL SERVICE(partyFinishBase64)(JNIEnv* env, jclass cls, jlong
     throw_arg(env, "five field arrays: secretShares, rShares, vShares, wShares, uShares");
     return;
   }
-  if (pin_all(env, pins, 5)) return;
+  const int staged = total_len(pins, 5) > region_bytes();
+  if (staged ? stage_native(env, pins, 5, 0) : pin_all(env, pins, 5)) return;
   char* ptrs[5];
   size_t lens[5];
   for (int k = 0; k < 5; ++k) {
@@ -596,7 +762,8 @@ JNIEXPORT void JNICALL SERVICE(partyFinishBase64)(JNIEnv* env, jclass cls, jlong
     lens[k] = (size_t)pins[k].len;
   }
   const int st = amphj_party_finish_b64(CTX(session), isPlayer0 ? 1 : 0, ptrs, lens);
-  unpin_all(env, pins, 5, 0);
+  if (staged) unstage_native(env, pins, 5, 0, st == AMPH_OK);
+  else unpin_all(env, pins, 5, 0);
   if (st != AMPH_OK) throw_status(env, st);
 }
 

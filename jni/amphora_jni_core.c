@@ -5,6 +5,10 @@
 #include <string.h>
 
 static __thread char g_msg[1024];
+/* AMPH_F_HOST_IO for this thread's next calls (amphj_set_host_io) */
+static __thread uint32_t g_io;
+
+void amphj_set_host_io(int on) { g_io = on ? AMPH_F_HOST_IO : 0u; }
 
 static int set_msg(int status, const char* msg) {
   snprintf(g_msg, sizeof g_msg, "%s", msg);
@@ -84,7 +88,7 @@ int amphj_recombine_verify(void* ctx, int n, const uint8_t* const* fields, const
   if (room(out_len, 16 * W, "the secrets array")) return AMPH_E_LEN;
   amph_odo odos[AMPH_MAX_PARTIES];
   odo_structs(n, fields, lens[0], odos);
-  return abi(amph_recombine_verify((amph_ctx*)ctx, odos, n, out, fail, 0, NULL));
+  return abi(amph_recombine_verify((amph_ctx*)ctx, odos, n, out, fail, g_io, NULL));
 }
 
 int amphj_mask_input(void* ctx, int n, const uint8_t* const* fields, const size_t* lens,
@@ -98,7 +102,7 @@ int amphj_mask_input(void* ctx, int n, const uint8_t* const* fields, const size_
   if (room(out_len, 16 * S, "the masked-input array")) return AMPH_E_LEN;
   amph_odo odos[AMPH_MAX_PARTIES];
   odo_structs(n, fields, lens[0], odos);
-  return abi(amph_mask_input((amph_ctx*)ctx, odos, n, secrets, S, out, fail, 0, NULL));
+  return abi(amph_mask_input((amph_ctx*)ctx, odos, n, secrets, S, out, fail, g_io, NULL));
 }
 
 int amphj_recombine(void* ctx, int n, const uint8_t* const* shares, const size_t* lens, uint8_t* out,
@@ -108,14 +112,14 @@ int amphj_recombine(void* ctx, int n, const uint8_t* const* shares, const size_t
   for (int j = 1; j < n; ++j)
     if (lens[j] / 16 < W) return set_msg(AMPH_E_LEN, kSameLength);
   if (room(out_len, 16 * W, "the output array")) return AMPH_E_LEN;
-  return abi(amph_recombine((amph_ctx*)ctx, shares, n, 16 * W, out, 0, NULL));
+  return abi(amph_recombine((amph_ctx*)ctx, shares, n, 16 * W, out, g_io, NULL));
 }
 
 int amphj_verify(void* ctx, const uint8_t* const* a, const size_t* lens, int64_t* fail) {
   *fail = -1;
   for (int k = 1; k < 5; ++k)
     if (lens[k] != lens[0]) return set_msg(AMPH_E_LEN, "verifySecrets: lists of unequal size");
-  return abi(amph_verify((amph_ctx*)ctx, a[0], a[1], a[2], a[3], a[4], lens[0] / 16, fail, 0, NULL));
+  return abi(amph_verify((amph_ctx*)ctx, a[0], a[1], a[2], a[3], a[4], lens[0] / 16, fail, g_io, NULL));
 }
 
 int amphj_mask_words(void* ctx, const uint8_t* secrets, size_t s_len, const uint8_t* masks, size_t m_len,
@@ -123,7 +127,7 @@ int amphj_mask_words(void* ctx, const uint8_t* secrets, size_t s_len, const uint
   const size_t W = s_len / 16;
   if (m_len / 16 != W) return set_msg(AMPH_E_LEN, "one input mask per secret word");
   if (room(out_len, 16 * W, "the output array")) return AMPH_E_LEN;
-  return abi(amph_mask_words((amph_ctx*)ctx, secrets, masks, W, out, 0, NULL));
+  return abi(amph_mask_words((amph_ctx*)ctx, secrets, masks, W, out, g_io, NULL));
 }
 
 int amphj_mask_word(void* ctx, const uint8_t secret[16], const uint8_t mask[16], uint8_t out[16]) {
@@ -185,7 +189,7 @@ int amphj_convert_share(void* ctx, const uint8_t* masked, size_t masked_len, con
     return set_msg(AMPH_E_LEN, "Received more input data than available inputMasks.");
   if (key_len != 16) return set_msg(AMPH_E_PARAM, "the MAC key must be a 16-byte little-endian integer");
   if (room(out_len, 32 * W, "the share array")) return AMPH_E_LEN;
-  return abi(amph_convert_share((amph_ctx*)ctx, masked, tuples, W, mac_key_le, use_zero_input_as_data, out, 0, NULL));
+  return abi(amph_convert_share((amph_ctx*)ctx, masked, tuples, W, mac_key_le, use_zero_input_as_data, out, g_io, NULL));
 }
 
 int amphj_odo_pre(void* ctx, const uint8_t* share, size_t share_len, int stride, const uint8_t* masks,
@@ -199,7 +203,7 @@ int amphj_odo_pre(void* ctx, const uint8_t* share, size_t share_len, int stride,
       room(out_len, 16 * W, "an ODO field array") || room(mag_len, 64 * W, "the diff magnitudes") ||
       room(neg_len, 4 * W, "the diff signs"))
     return AMPH_E_LEN;
-  return abi(amph_odo_pre((amph_ctx*)ctx, share, (size_t)stride, masks, triples, W, y, r, v, mag, neg, 0,
+  return abi(amph_odo_pre((amph_ctx*)ctx, share, (size_t)stride, masks, triples, W, y, r, v, mag, neg, g_io,
                           NULL));
 }
 
@@ -212,7 +216,7 @@ int amphj_open_post(void* ctx, int n, const uint8_t* const* mags, const size_t* 
     if (room(mag_lens[j], 64 * W, "a party's diff magnitudes") || room(neg_lens[j], 4 * W, "a party's diff signs"))
       return AMPH_E_LEN;
   if (room(out_len, 16 * W, "an ODO field array")) return AMPH_E_LEN;
-  return abi(amph_open_post((amph_ctx*)ctx, mags, negs, n, triples, W, is_player0, w, u, 0, NULL));
+  return abi(amph_open_post((amph_ctx*)ctx, mags, negs, n, triples, W, is_player0, w, u, g_io, NULL));
 }
 
 size_t amphj_exchange_max_chars(size_t npairs) { return amph_exchange_max_chars(npairs); }

@@ -27,6 +27,12 @@
 extern "C" {
 #endif
 
+/* Region mode for this thread's following calls (amphora_jni.c): the data
+ * pointers of recombine_verify, mask_input, recombine, verify, mask_words,
+ * convert_share (not its key), odo_pre and open_post are amph_host_array
+ * descriptors, passed with AMPH_F_HOST_IO.  Lengths are still the arrays'. */
+void amphj_set_host_io(int on);
+
 /* JNI class names ("/"-separated), or NULL for AMPH_OK */
 const char* amphj_exception_class(int status);
 const char* amphj_message(void);

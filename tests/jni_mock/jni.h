@@ -8,6 +8,8 @@
  * other JNI function is called inside a Get/ReleasePrimitiveArrayCritical
  * region, that at most 16 local references (or what EnsureLocalCapacity
  * reserved) are live in one native call, and lets a test make a pin fail.
+ * The JavaVM half (GetEnv / AttachCurrentThreadAsDaemon) lets the region-copy
+ * callbacks run on libamphora_hip's staging threads, which attach as daemons.
  * The real build (jni/Makefile) uses $JAVA_HOME/include/jni.h.
  */
 #ifndef JNI_MOCK_H_
@@ -20,6 +22,9 @@
 #define JNI_FALSE 0
 #define JNI_TRUE 1
 #define JNI_ABORT 2
+#define JNI_OK 0
+#define JNI_EDETACHED (-2)
+#define JNI_VERSION_1_6 0x00010006
 
 typedef int32_t jint;
 typedef int64_t jlong;
@@ -37,6 +42,13 @@ typedef jarray jobjectArray;
 
 struct JNINativeInterface_;
 typedef const struct JNINativeInterface_* JNIEnv;
+struct JNIInvokeInterface_;
+typedef const struct JNIInvokeInterface_* JavaVM;
+
+struct JNIInvokeInterface_ {
+  jint (*GetEnv)(JavaVM*, void**, jint);
+  jint (*AttachCurrentThreadAsDaemon)(JavaVM*, void**, void*);
+};
 
 struct JNINativeInterface_ {
   jclass (*FindClass)(JNIEnv*, const char*);
@@ -51,6 +63,11 @@ struct JNINativeInterface_ {
   jbyteArray (*NewByteArray)(JNIEnv*, jsize);
   jstring (*NewStringUTF)(JNIEnv*, const char*);
   jint (*EnsureLocalCapacity)(JNIEnv*, jint);
+  jint (*GetJavaVM)(JNIEnv*, JavaVM**);
+  jobject (*NewGlobalRef)(JNIEnv*, jobject);
+  void (*DeleteGlobalRef)(JNIEnv*, jobject);
+  jboolean (*ExceptionCheck)(JNIEnv*);
+  void (*ExceptionClear)(JNIEnv*);
 };
 
 #endif /* JNI_MOCK_H_ */

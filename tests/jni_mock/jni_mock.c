@@ -26,7 +26,7 @@ struct mock_obj {
 
 static struct mock_obj* g_all;
 static int g_critical;    /* open critical regions */
-static int g_violations;  /* JNI calls made inside one */
+static int g_violations;  /* JNI calls made inside one (or from an unattached thread) */
 static char g_exc_class[256];
 static char g_exc_msg[1024];
 static int g_local;          /* local references made in this native call */
@@ -34,6 +34,12 @@ static int g_capacity = 16;  /* the JNI guarantee, or what EnsureLocalCapacity r
 static int g_ref_overflows;  /* local references beyond it */
 static int g_fail_pin;       /* > 0: the g_fail_pin-th pin from now returns NULL */
 static int g_pins;           /* critical pins taken since mock_clear */
+/* region-copy callbacks run on the library's staging threads: atomics */
+static long g_region_copies; /* Get/SetByteArrayRegion calls since mock_clear */
+static int g_attaches;       /* threads attached to the mock VM */
+static int g_global_refs;    /* live global references */
+static int g_foreign_regions; /* region copies made on threads other than mock_env()'s */
+static __thread int t_attached;
 
 static struct mock_obj* obj_new(int kind, jsize len, size_t elem) {
   struct mock_obj* o = (struct mock_obj*)calloc(1, sizeof *o);
@@ -117,15 +123,31 @@ static void m_GetIntArrayRegion(JNIEnv* env, jintArray a, jsize start, jsize len
   memcpy(buf, (jint*)a->data + start, (size_t)len * sizeof(jint));
 }
 
+static void region_call(void) {
+  __atomic_fetch_add(&g_region_copies, 1, __ATOMIC_RELAXED);
+  if (!t_attached) __atomic_fetch_add(&g_violations, 1, __ATOMIC_RELAXED); /* JNI from an unattached thread */
+  if (t_attached == 2) __atomic_fetch_add(&g_foreign_regions, 1, __ATOMIC_RELAXED);
+}
+
 static void m_GetByteArrayRegion(JNIEnv* env, jbyteArray a, jsize start, jsize len, jbyte* buf) {
   (void)env;
   outside_critical();
+  region_call();
+  if (start < 0 || len < 0 || start + len > a->len) {
+    pending("java/lang/ArrayIndexOutOfBoundsException", "mock: region outside the array");
+    return;
+  }
   memcpy(buf, (jbyte*)a->data + start, (size_t)len);
 }
 
 static void m_SetByteArrayRegion(JNIEnv* env, jbyteArray a, jsize start, jsize len, const jbyte* buf) {
   (void)env;
   outside_critical();
+  region_call();
+  if (start < 0 || len < 0 || start + len > a->len) {
+    pending("java/lang/ArrayIndexOutOfBoundsException", "mock: region outside the array");
+    return;
+  }
   memcpy((jbyte*)a->data + start, buf, (size_t)len);
 }
 
@@ -153,16 +175,75 @@ static jint m_EnsureLocalCapacity(JNIEnv* env, jint n) {
   return 0;
 }
 
+static JNIEnv g_env;
+static JavaVM g_vm;
+
+static jint m_GetJavaVM(JNIEnv* env, JavaVM** vm) {
+  (void)env;
+  outside_critical();
+  *vm = &g_vm;
+  return 0;
+}
+
+static jobject m_NewGlobalRef(JNIEnv* env, jobject o) {
+  (void)env;
+  outside_critical();
+  __atomic_fetch_add(&g_global_refs, 1, __ATOMIC_RELAXED);
+  return o;
+}
+
+static void m_DeleteGlobalRef(JNIEnv* env, jobject o) {
+  (void)env;
+  (void)o;
+  outside_critical();
+  __atomic_fetch_sub(&g_global_refs, 1, __ATOMIC_RELAXED);
+}
+
+static jboolean m_ExceptionCheck(JNIEnv* env) {
+  (void)env;
+  return g_exc_class[0] ? JNI_TRUE : JNI_FALSE;
+}
+
+static void m_ExceptionClear(JNIEnv* env) {
+  (void)env;
+  g_exc_class[0] = g_exc_msg[0] = 0;
+}
+
+static jint vm_GetEnv(JavaVM* vm, void** penv, jint version) {
+  (void)vm;
+  (void)version;
+  if (!t_attached) return JNI_EDETACHED;
+  *penv = &g_env;
+  return JNI_OK;
+}
+
+static jint vm_AttachCurrentThreadAsDaemon(JavaVM* vm, void** penv, void* args) {
+  (void)vm;
+  (void)args;
+  if (!t_attached) {
+    t_attached = 2; /* a native thread the layer attached */
+    __atomic_fetch_add(&g_attaches, 1, __ATOMIC_RELAXED);
+  }
+  *penv = &g_env;
+  return JNI_OK;
+}
+
 static const struct JNINativeInterface_ g_table = {
     m_FindClass,          m_ThrowNew,          m_GetArrayLength,     m_GetObjectArrayElement,
     m_GetPrimitiveArrayCritical, m_ReleasePrimitiveArrayCritical, m_GetIntArrayRegion,
     m_GetByteArrayRegion, m_SetByteArrayRegion, m_NewByteArray,      m_NewStringUTF,
-    m_EnsureLocalCapacity,
+    m_EnsureLocalCapacity, m_GetJavaVM,        m_NewGlobalRef,       m_DeleteGlobalRef,
+    m_ExceptionCheck,     m_ExceptionClear,
 };
+static const struct JNIInvokeInterface_ g_vm_table = {vm_GetEnv, vm_AttachCurrentThreadAsDaemon};
 static JNIEnv g_env = &g_table;
+static JavaVM g_vm = &g_vm_table;
 
 /* ---- harness API (ctypes) ---- */
-JNIEXPORT JNIEnv* mock_env(void) { return &g_env; }
+JNIEXPORT JNIEnv* mock_env(void) {
+  t_attached = 1; /* the "Java" thread that calls the entry points */
+  return &g_env;
+}
 
 JNIEXPORT jobject mock_bytes(const uint8_t* data, jsize len) {
   struct mock_obj* o = obj_new(KIND_BYTES, len, 1);
@@ -193,6 +274,10 @@ JNIEXPORT int mock_open_criticals(void) { return g_critical; }
 JNIEXPORT int mock_ref_overflows(void) { return g_ref_overflows; }
 JNIEXPORT void mock_fail_pin(int k) { g_fail_pin = k; }
 JNIEXPORT int mock_pins(void) { return g_pins; }
+JNIEXPORT long mock_region_copies(void) { return __atomic_load_n(&g_region_copies, __ATOMIC_RELAXED); }
+JNIEXPORT int mock_foreign_regions(void) { return __atomic_load_n(&g_foreign_regions, __ATOMIC_RELAXED); }
+JNIEXPORT int mock_attaches(void) { return __atomic_load_n(&g_attaches, __ATOMIC_RELAXED); }
+JNIEXPORT int mock_global_refs(void) { return __atomic_load_n(&g_global_refs, __ATOMIC_RELAXED); }
 
 JNIEXPORT void mock_clear(void) {
   g_exc_class[0] = g_exc_msg[0] = 0;
@@ -202,6 +287,8 @@ JNIEXPORT void mock_clear(void) {
   g_ref_overflows = 0;
   g_fail_pin = 0;
   g_pins = 0;
+  __atomic_store_n(&g_region_copies, 0, __ATOMIC_RELAXED);
+  __atomic_store_n(&g_foreign_regions, 0, __ATOMIC_RELAXED);
 }
 
 JNIEXPORT void mock_free_all(void) {

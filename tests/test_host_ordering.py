@@ -47,9 +47,10 @@ def test_async_copies_only_in_the_pinned_pipeline():
         assert owner and owner[-1] == "run_batched_impl", \
             "hipMemcpyAsync outside the page-locked pipeline at offset %d (%s)" % (pos, owner)
     body = next(code[a:b] for n, a, b in spans if n == "run_batched_impl")
-    # host operands: the caller's buffer only when it is page-locked, else the slot's pinned buffer
-    assert "in_pinned[k] = amph::is_pinned_host(ins[k].host)" in body
-    assert "out_pinned[k] = amph::is_pinned_host(outs[k].host)" in body
+    # host operands: the caller's buffer only when it is page-locked, else the slot's pinned
+    # buffer (always for AMPH_F_HOST_IO arrays, which are callbacks, not memory)
+    assert "in_pinned[k] = !ins[k].io && amph::is_pinned_host(ins[k].host)" in body
+    assert "out_pinned[k] = !outs[k].io && amph::is_pinned_host(outs[k].host)" in body
     assert "hipMallocAsync" not in code, "stream-ordered staging is not used for host calls"
 
 

@@ -45,6 +45,7 @@ def J():
     L.mock_data.restype = vp
     L.mock_data.argtypes = [vp]
     L.mock_commits.argtypes = L.mock_aborts.argtypes = [vp]
+    L.mock_region_copies.restype = C.c_long
     L.mock_exception_class.restype = L.mock_exception_message.restype = C.c_char_p
     L.amphj_exception_class.restype = C.c_char_p
     return L
@@ -362,7 +363,8 @@ def test_service_party_session_three_parties(J, jctx, F):
         h = e.call(SERVICE + "partyBegin", C.c_int64, ctx, share_arr, C.c_int32(32), e.bytes(masks[j]),
                    e.bytes(triples[j]), C.c_int32(n), *fields)
         assert h != 0 and e.exception() is None and e.clean()
-        assert J.mock_aborts(share_arr) == 1 and J.mock_commits(share_arr) == 0
+        if os.environ.get("AMPH_JNI_REGION_BYTES") != "0":  # pinned: inputs released unwritten
+            assert J.mock_aborts(share_arr) == 1 and J.mock_commits(share_arr) == 0
         if j < 2:
             assert [e.read(x) for x in fields] == [pre[j][k].tobytes() for k in range(3)]
         txt = e.call(SERVICE + "partyText", C.c_void_p, C.c_int64(h))
@@ -429,3 +431,58 @@ def test_mask_word_makes_no_launch(J):
     assert e.call(CLIENT + "maskWord", C.c_void_p, C.c_int64(h), e.bytes(b"\1" * 8), e.bytes(le16(1))) is None
     assert e.exception() == (IAE, "maskWord takes two 16-byte words") and e.clean()
     Env(J).call(CLIENT + "ctxDestroy", None, C.c_int64(h))
+
+
+# ---- large calls: region copies, no critical region across the GPU call -------
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,W", [(2, 70_000), (3, 300_000)])
+def test_client_entry_points_region_mode(J, jctx, F, n, W, monkeypatch):
+    """above AMPH_JNI_REGION_BYTES (forced to 0 here) the
+    client entry points pin nothing: libamphora_hip's staging threads move
+    each batch with Get/SetByteArrayRegion (AMPH_F_HOST_IO), attached to the
+    VM as daemons; every result still equals the oracle's, and every global
+    reference is released."""
+    monkeypatch.setenv("AMPH_JNI_REGION_BYTES", "0")
+    J.mock_clear()
+    test_client_entry_points(J, jctx, F, n, W)
+    assert J.mock_pins() == 0, "a critical region was opened above the threshold"
+    assert J.mock_region_copies() > 0 and J.mock_global_refs() == 0
+    if 16 * W * (5 * n + 1) > (2 << 20):  # the batched pipeline: copies on the staging threads
+        assert J.mock_foreign_regions() > 0 and J.mock_attaches() > 0
+    assert J.mock_violations() == 0 and J.mock_open_criticals() == 0
+
+
+@pytest.mark.gpu
+def test_service_entry_points_region_mode(J, jctx, F, monkeypatch):
+    monkeypatch.setenv("AMPH_JNI_REGION_BYTES", "0")
+    J.mock_clear()
+    test_service_entry_points_two_party_output_delivery(J, jctx, F)
+    # exchangeEncode / exchangeDecode keep their (short, text-sized) pins; the
+    # word-array calls convertShare / odoPre / openPost took none
+    assert J.mock_global_refs() == 0 and J.mock_violations() == 0 and J.mock_open_criticals() == 0
+    assert J.mock_region_copies() > 0
+
+
+@pytest.mark.gpu
+def test_party_session_region_mode(J, jctx, F, monkeypatch):
+    """above the threshold the session calls copy their arrays
+    into native buffers with region copies -- nothing stays pinned while a
+    session call waits for the context or the GPU."""
+    monkeypatch.setenv("AMPH_JNI_REGION_BYTES", "0")
+    J.mock_clear()
+    test_service_party_session_three_parties(J, jctx, F)
+    assert J.mock_pins() == 0 and J.mock_open_criticals() == 0 and J.mock_violations() == 0
+
+
+@pytest.mark.gpu
+def test_small_calls_still_pin(J, jctx, F, monkeypatch):
+    """Below the default threshold (2 MiB of arrays) a call pins: short
+    critical regions are cheaper than region copies."""
+    monkeypatch.delenv("AMPH_JNI_REGION_BYTES", raising=False)
+    J.mock_clear()
+    e = Env(J)
+    odos, _ = F.synth_odos(seed=3, n=2, W=1000)
+    out = e.zeros(16 * 1000)
+    assert e.call(CLIENT + "recombineVerify", C.c_int64, C.c_int64(jctx), *e.odo_lists(odos), out) == -1
+    assert e.read(out) == F.recombine_verify(odos)[0].tobytes()
+    assert J.mock_pins() == 11 and J.mock_region_copies() == 0 and e.clean()
