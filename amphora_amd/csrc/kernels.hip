@@ -20,77 +20,11 @@
 
 #include "b64.hpp"
 #include "decimal.hpp"
+#include "devio.hpp"
 
 namespace amph {
 
-// Every launch goes through hipExtLaunchKernelGGL: with the config's timing
-// events set (amph_time_next_launch) the events are stamped by the kernel's
-// own dispatch, i.e. they measure the kernel, not the queue gap before it.
-#define AMPH_LAUNCH(K, G, B, C, ...) \
-  hipExtLaunchKernelGGL(K, G, B, 0, (C).stream, (C).ev_start, (C).ev_stop, 0, __VA_ARGS__)
-
 namespace {
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-// Streamed-once inputs: nontemporal 16-byte loads (global_load_dwordx4 nt;
-// AMPH_LD_NT=0 for A/B: plain loads measured 8-10 % slower at C2 with the
-// nontemporal stores in place).
-#ifndef AMPH_LD_NT
-#define AMPH_LD_NT 1
-#endif
-__device__ __forceinline__ uint4 ld(const uint4* p) {
-  if constexpr (AMPH_LD_NT) {
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-  } else {
-    return *p;
-  }
-}
-__device__ __forceinline__ void st(uint4* p, const W4& v) { *p = u4(v); }
-// Result words (K_RV / K_MASK and their wire forms, the open, the products):
-// nontemporal 16-byte stores.  Measured in bench.py on one box, alternating
-// builds 3x: C2 14.6-15.0 -> 15.6-15.8 G words/s, C3 10.7-10.8 -> 11.0-11.2;
-// k_open / k_open_post -7 % at 16 Mi words (profiles/r02_ab_store_policy.txt).
-// Plain stores left each kernel's output dirty in the caches for the next
-// launch to drain.  (Round 1's ubench_store had preferred plain stores at
-// 16 Mi words.)  Intermediates read again at once (K_ODO_PRE's diffs) keep
-// plain stores.
-#ifndef AMPH_ST_NT
-#define AMPH_ST_NT 1
-#endif
-__device__ __forceinline__ void st_out(uint4* p, const W4& v) {
-  if constexpr (AMPH_ST_NT) {
-    const uint4 x = u4(v);
-    __builtin_nontemporal_store(u32x4{x.x, x.y, x.z, x.w}, reinterpret_cast<u32x4*>(p));
-  } else {
-    *p = u4(v);
-  }
-}
-
-// Party-side outputs that the next stage reads at once (K_CONV's share
-// words, K_ODO_PRE's raw copies and diffs): nontemporal as well.  Alternated
-// A/B, 3x on one box: K_CONV and K_ODO_PRE -4 % at 16 Mi words, the exchange
-// encode that reads the diffs -8 %, party Output Delivery 4 Mi x 3
-// 1.81 -> 1.79 ms (profiles/r02_ab_store_policy.txt).  AMPH_PARTY_NT=0 for
-// plain stores.
-#ifndef AMPH_PARTY_NT
-#define AMPH_PARTY_NT 1
-#endif
-__device__ __forceinline__ void st_party(uint4* p, const uint4& x) {
-  if constexpr (AMPH_PARTY_NT) __builtin_nontemporal_store(u32x4{x.x, x.y, x.z, x.w}, reinterpret_cast<u32x4*>(p));
-  else *p = x;
-}
-
-// Wave-level reduction of the failing indices to one atomic per wave: the
-// lowest set lane holds the smallest index of this iteration.
-__device__ __forceinline__ void report_fail(bool bad, size_t i, unsigned long long* ff) {
-  const unsigned long long m = __ballot(bad);
-  if (m != 0ULL) {
-    const int lane = __lane_id();
-    if (lane == __ffsll((long long)m) - 1) atomicMin(ff, (unsigned long long)i);
-  }
-}
 
 // Sum over parties of one field at word i, canonical Montgomery form.
 template <int NP, bool BIG>
@@ -624,235 +558,6 @@ __global__ __launch_bounds__(kMaxBlock) void k_synth(OutSet out, int n, size_t w
   }
 }
 
-// ---- fused wire-format kernels ----------------------------------------------
-// The client receives each party's ODO as base64 text (VerifiableSecretShare /
-// OutputDeliveryObject JSON, Jackson's Base64Variants.MIME_NO_LINEFEEDS) and
-// sends each masked word as a 24-character record (MaskedInputData).  Decoding
-// the 5N fields to HBM and then running K_RV / K_MASK moves 4/3 x 80N + 2 x 80N
-// bytes per word; these kernels decode the text in the workgroup and consume
-// it from LDS, so the decoded words never reach HBM (K_RV from text: 4/3 x
-// 80N + 16 B/word).
-//
-// A workgroup of kWireBlock lanes owns 16 x kWireBlock characters of every
-// field = 12 x kWireBlock bytes = kWireWords words.  Per field every lane
-// decodes one 16-character unit (4 groups) and writes its 12 bytes to LDS;
-// after a barrier the first kWireWords lanes (whole waves: the last quarter of
-// the waves only decode) read their 16-byte word and add it into the field's
-// sum.  Two LDS buffers alternate, so one barrier per field suffices.  The
-// text's final group may carry '=' padding: the workgroup that holds it
-// (or any character past the text) takes the per-character path.
-constexpr int kWireBlock = 256;  // workgroup size: 256 > 512 > 1024 by 15-50 % (tools/ubench/ubench_wire.hip)
-template <int BS>
-struct Wire {
-  static constexpr int words = BS * 3 / 4;          // words per workgroup
-  static constexpr size_t chars = (size_t)16 * BS;  // characters per field per workgroup
-};
-
-// One 16-character unit of a field's text, checked character by character:
-// positions >= nchars decode as 'A' (zero bits, beyond the last word);
-// the final `pad` positions must be '=' (decoded as 'A'), '=' anywhere else
-// is invalid like any non-alphabet character.  Returns the unit's first
-// invalid offset (or 0xFFFFFFFF) and its 12 bytes in o.
-__device__ __forceinline__ uint32_t dec_unit_slow(const char* t, size_t unit, size_t nchars,
-                                                  uint32_t pad, uint32_t (&o)[3]) {
-  uint32_t w[4] = {0, 0, 0, 0}, forced = 0xFFFFFFFFu;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const size_t pos = 16 * unit + q;
-    uint32_t ch = pos < nchars ? (uint8_t)t[pos] : (uint32_t)'A';
-    if (pos < nchars && pos + pad >= nchars) {
-      if (ch != '=' && forced == 0xFFFFFFFFu) forced = q;
-      ch = 'A';
-    }
-    w[q >> 2] |= ch << (8 * (q & 3));
-  }
-  const uint32_t fb = dec_unit16(make_uint4(w[0], w[1], w[2], w[3]), o);
-  return min(fb, forced);
-}
-
-// Sum field k over the parties from the text, consuming it through LDS.  raw:
-// this lane's units, loaded up front on the fast path (FAST).
-// Fast-path loads: kWirePrefetch > 0 issues field f + kWirePrefetch's load
-// while field f is decoded (fewer live VGPRs); 0 issues all 5N up front.
-#ifndef AMPH_WIRE_PD
-#define AMPH_WIRE_PD 0
-#endif
-constexpr int kWirePrefetch = AMPH_WIRE_PD;
-
-// Fields decoded per barrier (AMPH_WIRE_G): G units of text go to LDS before
-// each barrier (2G buffers alternate, or all 5N at once, one barrier in all,
-// when G >= 5N).
-#ifndef AMPH_WIRE_G
-#define AMPH_WIRE_G 5  // 2-5 % over 1 at 1 and 16 Mi words (profiles/r02_ubench_wire_groups.txt)
-#endif
-template <int NP>
-struct WireGroups {
-  static constexpr int F = 5 * (NP > 0 ? NP : 1);  // fields (runtime party counts: G = 1)
-  static constexpr int G = NP > 0 ? (AMPH_WIRE_G < F ? AMPH_WIRE_G : F) : 1;
-  static constexpr int bufs = G >= F ? F : 2 * G;
-};
-
-template <int NP, bool BIG, bool FAST, int BS>
-__device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nchars, uint32_t pad,
-                                            size_t words, uint4 (&raw)[5][NP > 0 ? NP : 1],
-                                            uint32_t (*lds)[3 * BS], W4 (&acc)[5],
-                                            unsigned long long* bad, const Fp& f) {
-  constexpr int G = WireGroups<NP>::G, NB = WireGroups<NP>::bufs;
-  const size_t unit = (size_t)blockIdx.x * BS + threadIdx.x;
-  const size_t word = (size_t)blockIdx.x * Wire<BS>::words + threadIdx.x;
-  const bool consumer = threadIdx.x < Wire<BS>::words && word < words;
-  const int np = NP > 0 ? NP : n;
-  int slot = 0;  // LDS buffer of the next field
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-#pragma unroll
-    for (int j = 0; j < (NP > 0 ? NP : kMaxParties); ++j) {
-      if (NP == 0 && j >= np) break;
-      uint32_t o[3];
-      uint32_t fb;
-      if constexpr (FAST && NP > 0) {
-        if constexpr (kWirePrefetch > 0) {
-          const int ahead = k * NP + j + kWirePrefetch;
-          if (ahead < 5 * NP)
-            raw[ahead / NP][ahead % NP] = ld(reinterpret_cast<const uint4*>(tx.t[ahead / NP][ahead % NP]) + unit);
-        }
-        fb = dec_unit16(raw[k][j], o);
-      } else if constexpr (FAST) {
-        fb = dec_unit16(ld(reinterpret_cast<const uint4*>(tx.t[k][j]) + unit), o);
-      } else {
-        fb = dec_unit_slow(tx.t[k][j], unit, nchars, pad, o);
-      }
-      if (fb != 0xFFFFFFFFu)  // (party j, field k) in ODO order, then the offset
-        atomicMin(bad, (unsigned long long)((size_t)(5 * j + k) * nchars + 16 * unit + fb));
-      uint32_t* l = lds[slot];
-      l[3 * threadIdx.x] = o[0];
-      l[3 * threadIdx.x + 1] = o[1];
-      l[3 * threadIdx.x + 2] = o[2];
-      const int fi = k * (NP > 0 ? NP : 1) + j;  // flat field index (G = 1 for runtime counts)
-      const bool group_end = G == 1 || (fi + 1) % G == 0 || fi + 1 == WireGroups<NP>::F;
-      if (group_end) {
-        __syncthreads();
-        if (consumer) {
-          // the group's fields, oldest first: fields fi - m, m = cnt-1 .. 0
-          const int cnt = G == 1 ? 1 : (fi % G) + 1;
-#pragma unroll
-          for (int m = (G == 1 ? 0 : G - 1); m >= 0; --m) {
-            if (m >= cnt) continue;
-            const int ff = fi - m, kk = G == 1 ? k : ff / (NP > 0 ? NP : 1), jj = G == 1 ? j : ff % (NP > 0 ? NP : 1);
-            const int sl = (slot - m + NB) % NB;
-            const uint4 v = reinterpret_cast<const uint4*>(lds[sl])[threadIdx.x];
-            const W4 x = canon<BIG>(w4(v), f);
-            acc[kk] = jj == 0 ? x : mod_add(acc[kk], x, f);
-          }
-        }
-      }
-      slot = (slot + 1) % NB;
-    }
-  }
-}
-
-template <int NP, int BS>
-__device__ __forceinline__ void wire_load(const TextSet& tx, uint4 (&raw)[5][NP > 0 ? NP : 1]) {
-  if constexpr (NP > 0) {
-    const size_t unit = (size_t)blockIdx.x * BS + threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < 5; ++k)
-#pragma unroll
-      for (int j = 0; j < NP; ++j)
-        if (kWirePrefetch == 0 || k * NP + j < kWirePrefetch)
-          raw[k][j] = ld(reinterpret_cast<const uint4*>(tx.t[k][j]) + unit);
-  }
-}
-
-// K_RV from the wire: the N parties' base64 ODO fields -> canonical secrets,
-// MAC verify (getSecret, DefaultAmphoraClient.java:206-217 incl. the Jackson
-// base64 decode of every field).  bad: min (5 party + field) * nchars + offset
-// of an invalid character.
-template <int NP, bool BIG, int BS>
-__global__ __launch_bounds__(BS) void k_rv_b64(TextSet tx, int n, size_t words, size_t nchars,
-                                           uint32_t pad, uint4* out_y, unsigned long long* ff,
-                                           unsigned long long* bad, Fp f) {
-  __shared__ uint32_t lds[WireGroups<NP>::bufs < 2 ? 2 : WireGroups<NP>::bufs][3 * BS];
-  W4 acc[5];
-  uint4 raw[5][NP > 0 ? NP : 1];
-  const bool fast = ((size_t)blockIdx.x + 1) * Wire<BS>::chars + 4 <= nchars;
-  if (fast) {
-    wire_load<NP, BS>(tx, raw);
-    wire_fields<NP, BIG, true, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f);
-  } else {
-    wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f);
-  }
-  const size_t word = (size_t)blockIdx.x * Wire<BS>::words + threadIdx.x;
-  if (threadIdx.x < Wire<BS>::words) {  // whole waves
-    const bool in = word < words;
-    bool ok = true;
-    if (in) {
-      ok = (int)eq(mont_mul_v(acc[0], acc[1], f), acc[3]) & (int)eq(mont_mul_v(acc[2], acc[1], f), acc[4]);
-      st_out(out_y + word, redc(acc[0], f));
-    }
-    report_fail(in && !ok, word, ff);
-  }
-}
-
-// K_MASK from the wire: the N parties' base64 Input Mask ODO fields + the
-// secrets -> verify the masks, masked[i] = toGfp((s_i - m_i) mod p) for
-// i < n_secrets, written as raw words (out16) and/or as the 24-character
-// base64 records of MaskedInputData (out24, staged through LDS and stored as
-// coalesced 16-byte runs).  createSecret, DefaultAmphoraClient.java:150-170.
-template <int NP, bool BIG, int BS>
-__global__ __launch_bounds__(BS) void k_mask_b64(TextSet tx, int n, size_t words, size_t nchars,
-                                             uint32_t pad, const uint4* secrets, size_t n_secrets,
-                                             uint4* out16, char* out24, unsigned long long* ff,
-                                             unsigned long long* bad, Fp f) {
-  constexpr int WW = Wire<BS>::words;
-  __shared__ uint32_t lds[WireGroups<NP>::bufs < 2 ? 2 : WireGroups<NP>::bufs][3 * BS];
-  W4 acc[5];
-  uint4 raw[5][NP > 0 ? NP : 1];
-  const size_t word = (size_t)blockIdx.x * WW + threadIdx.x;
-  const bool has_secret = threadIdx.x < WW && word < n_secrets;
-  uint4 s = make_uint4(0, 0, 0, 0);
-  if (has_secret) s = ld(secrets + word);
-  const bool fast = ((size_t)blockIdx.x + 1) * Wire<BS>::chars + 4 <= nchars;
-  if (fast) {
-    wire_load<NP, BS>(tx, raw);
-    wire_fields<NP, BIG, true, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f);
-  } else {
-    wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f);
-  }
-  uint32_t g[6];
-  if (threadIdx.x < WW) {
-    const bool in = word < words;
-    bool ok = true;
-    if (in) ok = (int)eq(mont_mul_v(acc[0], acc[1], f), acc[3]) & (int)eq(mont_mul_v(acc[2], acc[1], f), acc[4]);
-    report_fail(in && !ok, word, ff);
-    if (has_secret) {
-      const uint4 m = u4(mod_sub(mont_mul_v(w4(s), r2_word(f), f), acc[0], f));
-      if (out16) st_out(out16 + word, w4(m));
-      enc_word24(m, g);
-    }
-  }
-  if (!out24) return;
-  // records: 24 B per word through LDS (the two decode buffers, 24 KiB), then
-  // the workgroup's run as 16-byte stores (full workgroups; the last one's
-  // tail per byte)
-  __syncthreads();
-  uint32_t* l = &lds[0][0];
-  if (has_secret)
-#pragma unroll
-    for (int q = 0; q < 6; ++q) l[6 * threadIdx.x + q] = g[q];
-  __syncthreads();
-  const size_t w0 = (size_t)blockIdx.x * WW;
-  const size_t nrec = w0 < n_secrets ? min((size_t)WW, n_secrets - w0) : 0;
-  char* dst = out24 + 24 * w0;
-  if (nrec == (size_t)WW) {
-    for (int q = threadIdx.x; q < 6 * WW / 4; q += BS)
-      reinterpret_cast<uint4*>(dst)[q] = make_uint4(l[4 * q], l[4 * q + 1], l[4 * q + 2], l[4 * q + 3]);
-  } else {
-    for (size_t q = threadIdx.x; q < 6 * nrec; q += BS)
-      reinterpret_cast<uint32_t*>(dst)[q] = l[q];
-  }
-}
-
 // Measurement only: K_MASK's exact memory pattern (the same 5N + 1 nontemporal
 // 16-B loads per lane, one 16-B store, same grid) with the field arithmetic
 // replaced by an XOR, so bench.py can time, in the same run and on the same
@@ -900,14 +605,6 @@ unsigned grid_for(size_t words, const LaunchCfg& c) {
 
 // Dispatch helpers: party count is a template parameter for 1..4 (the
 // configurations Amphora deploys), runtime loop above that.
-#define AMPH_DISPATCH_NP(n, BIG, LAUNCH) \
-  switch (n) {                           \
-    case 1: LAUNCH(1, BIG); break;       \
-    case 2: LAUNCH(2, BIG); break;       \
-    case 3: LAUNCH(3, BIG); break;       \
-    case 4: LAUNCH(4, BIG); break;       \
-    default: LAUNCH(0, BIG); break;      \
-  }
 
 }  // namespace
 
@@ -1074,31 +771,6 @@ hipError_t launch_synth_odos(const OutSet& out, int n, size_t words, uint64_t se
   const unsigned g = grid_for(words, c);
   if (f.big) AMPH_LAUNCH((k_synth<true>), dim3(g), dim3(c.block), c, out, n, words, seed, plain_y, fault, permille, f);
   else AMPH_LAUNCH((k_synth<false>), dim3(g), dim3(c.block), c, out, n, words, seed, plain_y, fault, permille, f);
-  return hipGetLastError();
-}
-
-hipError_t launch_rv_b64(const TextSet& tx, int n, size_t words, size_t nchars, uint32_t pad,
-                         uint4* out_y, unsigned long long* ff, unsigned long long* bad, const Fp& f,
-                         const LaunchCfg& c) {
-  if (words == 0) return hipSuccess;
-  constexpr int BS = kWireBlock;
-  const dim3 g((unsigned)((words + Wire<BS>::words - 1) / Wire<BS>::words));
-#define L(NP, BIG) AMPH_LAUNCH((k_rv_b64<NP, BIG, BS>), g, dim3(BS), c, tx, n, words, nchars, pad, out_y, ff, bad, f)
-  if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
-#undef L
-  return hipGetLastError();
-}
-
-hipError_t launch_mask_b64(const TextSet& tx, int n, size_t words, size_t nchars, uint32_t pad,
-                           const uint4* secrets, size_t n_secrets, uint4* out16, char* out24,
-                           unsigned long long* ff, unsigned long long* bad, const Fp& f,
-                           const LaunchCfg& c) {
-  if (words == 0) return hipSuccess;
-  constexpr int BS = kWireBlock;
-  const dim3 g((unsigned)((words + Wire<BS>::words - 1) / Wire<BS>::words));
-#define L(NP, BIG) AMPH_LAUNCH((k_mask_b64<NP, BIG, BS>), g, dim3(BS), c, tx, n, words, nchars, pad, secrets, n_secrets, out16, out24, ff, bad, f)
-  if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
-#undef L
   return hipGetLastError();
 }
 

@@ -1,0 +1,488 @@
+// The fused wire-format kernels: K_RV / K_MASK straight from the base64 text
+// of the ODO fields (getSecret / createSecret with Jackson's base64 decode of
+// every byte[] field, DefaultAmphoraClient.java:150-170,206-217), in two
+// forms -- round 2's LDS-transpose form and round 4's register form (the
+// default; AMPH_WIRE_FORM=lds for A/B).  Roofline: HBM (text + secrets +
+// outputs), see DESIGN.md §4a.
+#include <cstdlib>
+#include <string>
+
+#include "b64.hpp"
+#include "devio.hpp"
+
+namespace amph {
+namespace {
+
+// ---- fused wire-format kernels ----------------------------------------------
+// The client receives each party's ODO as base64 text (VerifiableSecretShare /
+// OutputDeliveryObject JSON, Jackson's Base64Variants.MIME_NO_LINEFEEDS) and
+// sends each masked word as a 24-character record (MaskedInputData).  Decoding
+// the 5N fields to HBM and then running K_RV / K_MASK moves 4/3 x 80N + 2 x 80N
+// bytes per word; these kernels decode the text in the workgroup and consume
+// it from LDS, so the decoded words never reach HBM (K_RV from text: 4/3 x
+// 80N + 16 B/word).
+//
+// A workgroup of kWireBlock lanes owns 16 x kWireBlock characters of every
+// field = 12 x kWireBlock bytes = kWireWords words.  Per field every lane
+// decodes one 16-character unit (4 groups) and writes its 12 bytes to LDS;
+// after a barrier the first kWireWords lanes (whole waves: the last quarter of
+// the waves only decode) read their 16-byte word and add it into the field's
+// sum.  Two LDS buffers alternate, so one barrier per field suffices.  The
+// text's final group may carry '=' padding: the workgroup that holds it
+// (or any character past the text) takes the per-character path.
+constexpr int kWireBlock = 256;  // workgroup size: 256 > 512 > 1024 by 15-50 % (tools/ubench/ubench_wire.hip)
+template <int BS>
+struct Wire {
+  static constexpr int words = BS * 3 / 4;          // words per workgroup
+  static constexpr size_t chars = (size_t)16 * BS;  // characters per field per workgroup
+};
+
+// One 16-character unit of a field's text, checked character by character:
+// positions >= nchars decode as 'A' (zero bits, beyond the last word);
+// the final `pad` positions must be '=' (decoded as 'A'), '=' anywhere else
+// is invalid like any non-alphabet character.  Returns the unit's first
+// invalid offset (or 0xFFFFFFFF) and its 12 bytes in o.
+__device__ __forceinline__ uint32_t dec_unit_slow(const char* t, size_t unit, size_t nchars,
+                                                  uint32_t pad, uint32_t (&o)[3]) {
+  uint32_t w[4] = {0, 0, 0, 0}, forced = 0xFFFFFFFFu;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const size_t pos = 16 * unit + q;
+    uint32_t ch = pos < nchars ? (uint8_t)t[pos] : (uint32_t)'A';
+    if (pos < nchars && pos + pad >= nchars) {
+      if (ch != '=' && forced == 0xFFFFFFFFu) forced = q;
+      ch = 'A';
+    }
+    w[q >> 2] |= ch << (8 * (q & 3));
+  }
+  const uint32_t fb = dec_unit16(make_uint4(w[0], w[1], w[2], w[3]), o);
+  return min(fb, forced);
+}
+
+// Sum field k over the parties from the text, consuming it through LDS.  raw:
+// this lane's units, loaded up front on the fast path (FAST).
+// Fast-path loads: kWirePrefetch > 0 issues field f + kWirePrefetch's load
+// while field f is decoded (fewer live VGPRs); 0 issues all 5N up front.
+#ifndef AMPH_WIRE_PD
+#define AMPH_WIRE_PD 0
+#endif
+constexpr int kWirePrefetch = AMPH_WIRE_PD;
+
+// Fields decoded per barrier (AMPH_WIRE_G): G units of text go to LDS before
+// each barrier (2G buffers alternate, or all 5N at once, one barrier in all,
+// when G >= 5N).
+#ifndef AMPH_WIRE_G
+#define AMPH_WIRE_G 5  // 2-5 % over 1 at 1 and 16 Mi words (profiles/r02_ubench_wire_groups.txt)
+#endif
+template <int NP>
+struct WireGroups {
+  static constexpr int F = 5 * (NP > 0 ? NP : 1);  // fields (runtime party counts: G = 1)
+  static constexpr int G = NP > 0 ? (AMPH_WIRE_G < F ? AMPH_WIRE_G : F) : 1;
+  static constexpr int bufs = G >= F ? F : 2 * G;
+};
+
+template <int NP, bool BIG, bool FAST, int BS>
+__device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nchars, uint32_t pad,
+                                            size_t words, uint4 (&raw)[5][NP > 0 ? NP : 1],
+                                            uint32_t (*lds)[3 * BS], W4 (&acc)[5],
+                                            unsigned long long* bad, const Fp& f) {
+  constexpr int G = WireGroups<NP>::G, NB = WireGroups<NP>::bufs;
+  const size_t unit = (size_t)blockIdx.x * BS + threadIdx.x;
+  const size_t word = (size_t)blockIdx.x * Wire<BS>::words + threadIdx.x;
+  const bool consumer = threadIdx.x < Wire<BS>::words && word < words;
+  const int np = NP > 0 ? NP : n;
+  int slot = 0;  // LDS buffer of the next field
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+#pragma unroll
+    for (int j = 0; j < (NP > 0 ? NP : kMaxParties); ++j) {
+      if (NP == 0 && j >= np) break;
+      uint32_t o[3];
+      uint32_t fb;
+      if constexpr (FAST && NP > 0) {
+        if constexpr (kWirePrefetch > 0) {
+          const int ahead = k * NP + j + kWirePrefetch;
+          if (ahead < 5 * NP)
+            raw[ahead / NP][ahead % NP] = ld(reinterpret_cast<const uint4*>(tx.t[ahead / NP][ahead % NP]) + unit);
+        }
+        fb = dec_unit16(raw[k][j], o);
+      } else if constexpr (FAST) {
+        fb = dec_unit16(ld(reinterpret_cast<const uint4*>(tx.t[k][j]) + unit), o);
+      } else {
+        fb = dec_unit_slow(tx.t[k][j], unit, nchars, pad, o);
+      }
+      if (fb != 0xFFFFFFFFu)  // (party j, field k) in ODO order, then the offset
+        atomicMin(bad, (unsigned long long)((size_t)(5 * j + k) * nchars + 16 * unit + fb));
+      uint32_t* l = lds[slot];
+      l[3 * threadIdx.x] = o[0];
+      l[3 * threadIdx.x + 1] = o[1];
+      l[3 * threadIdx.x + 2] = o[2];
+      const int fi = k * (NP > 0 ? NP : 1) + j;  // flat field index (G = 1 for runtime counts)
+      const bool group_end = G == 1 || (fi + 1) % G == 0 || fi + 1 == WireGroups<NP>::F;
+      if (group_end) {
+        __syncthreads();
+        if (consumer) {
+          // the group's fields, oldest first: fields fi - m, m = cnt-1 .. 0
+          const int cnt = G == 1 ? 1 : (fi % G) + 1;
+#pragma unroll
+          for (int m = (G == 1 ? 0 : G - 1); m >= 0; --m) {
+            if (m >= cnt) continue;
+            const int ff = fi - m, kk = G == 1 ? k : ff / (NP > 0 ? NP : 1), jj = G == 1 ? j : ff % (NP > 0 ? NP : 1);
+            const int sl = (slot - m + NB) % NB;
+            const uint4 v = reinterpret_cast<const uint4*>(lds[sl])[threadIdx.x];
+            const W4 x = canon<BIG>(w4(v), f);
+            acc[kk] = jj == 0 ? x : mod_add(acc[kk], x, f);
+          }
+        }
+      }
+      slot = (slot + 1) % NB;
+    }
+  }
+}
+
+template <int NP, int BS>
+__device__ __forceinline__ void wire_load(const TextSet& tx, uint4 (&raw)[5][NP > 0 ? NP : 1]) {
+  if constexpr (NP > 0) {
+    const size_t unit = (size_t)blockIdx.x * BS + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+      for (int j = 0; j < NP; ++j)
+        if (kWirePrefetch == 0 || k * NP + j < kWirePrefetch)
+          raw[k][j] = ld(reinterpret_cast<const uint4*>(tx.t[k][j]) + unit);
+  }
+}
+
+// K_RV from the wire: the N parties' base64 ODO fields -> canonical secrets,
+// MAC verify (getSecret, DefaultAmphoraClient.java:206-217 incl. the Jackson
+// base64 decode of every field).  bad: min (5 party + field) * nchars + offset
+// of an invalid character.
+template <int NP, bool BIG, int BS>
+__global__ __launch_bounds__(BS) void k_rv_b64(TextSet tx, int n, size_t words, size_t nchars,
+                                           uint32_t pad, uint4* out_y, unsigned long long* ff,
+                                           unsigned long long* bad, Fp f) {
+  __shared__ uint32_t lds[WireGroups<NP>::bufs < 2 ? 2 : WireGroups<NP>::bufs][3 * BS];
+  W4 acc[5];
+  uint4 raw[5][NP > 0 ? NP : 1];
+  const bool fast = ((size_t)blockIdx.x + 1) * Wire<BS>::chars + 4 <= nchars;
+  if (fast) {
+    wire_load<NP, BS>(tx, raw);
+    wire_fields<NP, BIG, true, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f);
+  } else {
+    wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f);
+  }
+  const size_t word = (size_t)blockIdx.x * Wire<BS>::words + threadIdx.x;
+  if (threadIdx.x < Wire<BS>::words) {  // whole waves
+    const bool in = word < words;
+    bool ok = true;
+    if (in) {
+      ok = (int)eq(mont_mul_v(acc[0], acc[1], f), acc[3]) & (int)eq(mont_mul_v(acc[2], acc[1], f), acc[4]);
+      st_out(out_y + word, redc(acc[0], f));
+    }
+    report_fail(in && !ok, word, ff);
+  }
+}
+
+// K_MASK from the wire: the N parties' base64 Input Mask ODO fields + the
+// secrets -> verify the masks, masked[i] = toGfp((s_i - m_i) mod p) for
+// i < n_secrets, written as raw words (out16) and/or as the 24-character
+// base64 records of MaskedInputData (out24, staged through LDS and stored as
+// coalesced 16-byte runs).  createSecret, DefaultAmphoraClient.java:150-170.
+template <int NP, bool BIG, int BS>
+__global__ __launch_bounds__(BS) void k_mask_b64(TextSet tx, int n, size_t words, size_t nchars,
+                                             uint32_t pad, const uint4* secrets, size_t n_secrets,
+                                             uint4* out16, char* out24, unsigned long long* ff,
+                                             unsigned long long* bad, Fp f) {
+  constexpr int WW = Wire<BS>::words;
+  __shared__ uint32_t lds[WireGroups<NP>::bufs < 2 ? 2 : WireGroups<NP>::bufs][3 * BS];
+  W4 acc[5];
+  uint4 raw[5][NP > 0 ? NP : 1];
+  const size_t word = (size_t)blockIdx.x * WW + threadIdx.x;
+  const bool has_secret = threadIdx.x < WW && word < n_secrets;
+  uint4 s = make_uint4(0, 0, 0, 0);
+  if (has_secret) s = ld(secrets + word);
+  const bool fast = ((size_t)blockIdx.x + 1) * Wire<BS>::chars + 4 <= nchars;
+  if (fast) {
+    wire_load<NP, BS>(tx, raw);
+    wire_fields<NP, BIG, true, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f);
+  } else {
+    wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f);
+  }
+  uint32_t g[6];
+  if (threadIdx.x < WW) {
+    const bool in = word < words;
+    bool ok = true;
+    if (in) ok = (int)eq(mont_mul_v(acc[0], acc[1], f), acc[3]) & (int)eq(mont_mul_v(acc[2], acc[1], f), acc[4]);
+    report_fail(in && !ok, word, ff);
+    if (has_secret) {
+      const uint4 m = u4(mod_sub(mont_mul_v(w4(s), r2_word(f), f), acc[0], f));
+      if (out16) st_out(out16 + word, w4(m));
+      enc_word24(m, g);
+    }
+  }
+  if (!out24) return;
+  // records: 24 B per word through LDS (the two decode buffers, 24 KiB), then
+  // the workgroup's run as 16-byte stores (full workgroups; the last one's
+  // tail per byte)
+  __syncthreads();
+  uint32_t* l = &lds[0][0];
+  if (has_secret)
+#pragma unroll
+    for (int q = 0; q < 6; ++q) l[6 * threadIdx.x + q] = g[q];
+  __syncthreads();
+  const size_t w0 = (size_t)blockIdx.x * WW;
+  const size_t nrec = w0 < n_secrets ? min((size_t)WW, n_secrets - w0) : 0;
+  char* dst = out24 + 24 * w0;
+  if (nrec == (size_t)WW) {
+    for (int q = threadIdx.x; q < 6 * WW / 4; q += BS)
+      reinterpret_cast<uint4*>(dst)[q] = make_uint4(l[4 * q], l[4 * q + 1], l[4 * q + 2], l[4 * q + 3]);
+  } else {
+    for (size_t q = threadIdx.x; q < 6 * nrec; q += BS)
+      reinterpret_cast<uint32_t*>(dst)[q] = l[q];
+  }
+}
+
+// ---- register form of the fused wire kernels (no LDS, no barrier) --------------
+// 64 characters of a field are exactly 48 bytes = 3 words, so a lane that owns
+// THREE consecutive words reads its 64 characters (four 16-byte loads, lanes
+// 64 B apart) and has every byte of its words in its own registers after the
+// decode: no LDS transpose, no barrier, every wave independent of the others.
+// Fields are consumed in the order y, r, w, v, u so that w is checked against
+// y r and dropped before v and u are summed (48 live accumulator registers
+// instead of 60); one field's four loads are issued before the previous
+// field's decode.
+constexpr int kWireRegBlock = 256;
+constexpr int kWireRegWords = 3;  // words per lane
+
+// one party's field: this lane's 64 characters (units 4 lane .. 4 lane + 3)
+// -> its three words.  FAST: full units, validity ANDed into okacc (the
+// offset of a bad character is searched for afterwards, wreg_find_bad);
+// otherwise per character (padding, the text's end) with the offset reported
+// at once.
+template <bool FAST>
+__device__ __forceinline__ void wreg_unit_words(const uint4 (&raw)[4], const char* t, size_t lane,
+                                                size_t nchars, uint32_t pad, int fieldno,
+                                                unsigned long long* bad, uint32_t& okacc,
+                                                W4 (&x)[kWireRegWords]) {
+  uint32_t o[12];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    uint32_t q[3];
+    if constexpr (FAST) {
+      dec_unit16_acc(raw[u], q, okacc);
+      // one unit at a time: interleaving the four units' 16 independent group
+      // decodes costs ~100 VGPRs for little VALU latency to hide
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      const size_t unit = 4 * lane + u;
+      const uint32_t fb = dec_unit_slow(t, unit, nchars, pad, q);
+      if (fb != 0xFFFFFFFFu) atomicMin(bad, (unsigned long long)((size_t)fieldno * nchars + 16 * unit + fb));
+    }
+    o[3 * u] = q[0];
+    o[3 * u + 1] = q[1];
+    o[3 * u + 2] = q[2];
+  }
+#pragma unroll
+  for (int m = 0; m < kWireRegWords; ++m) x[m] = W4{{o[4 * m], o[4 * m + 1], o[4 * m + 2], o[4 * m + 3]}};
+}
+
+// a lane whose characters were not all valid (okacc): the first bad offset
+// of every field, re-read one unit at a time (rare: a malformed response)
+__device__ __noinline__ void wreg_find_bad(const TextSet& tx, int n, size_t lane, size_t nchars, uint32_t pad,
+                                           unsigned long long* bad) {
+  for (int j = 0; j < n; ++j)
+    for (int k = 0; k < 5; ++k)
+      for (int u = 0; u < 4; ++u) {
+        uint32_t q[3];
+        const size_t unit = 4 * lane + u;
+        const uint32_t fb = dec_unit_slow(tx.t[k][j], unit, nchars, pad, q);
+        if (fb != 0xFFFFFFFFu) atomicMin(bad, (unsigned long long)((size_t)(5 * j + k) * nchars + 16 * unit + fb));
+      }
+}
+
+template <int NP, bool BIG, bool FAST>
+__device__ __forceinline__ void wreg_field(const TextSet& tx, int k, int n, size_t lane, size_t nchars,
+                                           uint32_t pad, unsigned long long* bad, uint32_t& okacc,
+                                           W4 (&acc)[kWireRegWords], const Fp& f) {
+  // A runtime loop over the parties (not unrolled): the compiler then cannot
+  // interleave several parties' or fields' decodes, which took every lane to
+  // 256 VGPRs (one wave per SIMD) when the whole verify was unrolled.  The
+  // next party's four loads are issued before this party's decode.
+  const int np = NP > 0 ? NP : n;
+  uint4 raw[4] = {};
+  if constexpr (FAST) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) raw[u] = ld(reinterpret_cast<const uint4*>(tx.t[k][0]) + 4 * lane + u);
+  }
+#pragma unroll 1
+  for (int j = 0; j < np; ++j) {
+    uint4 next[4] = {};
+    if constexpr (FAST) {
+      if (j + 1 < np)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) next[u] = ld(reinterpret_cast<const uint4*>(tx.t[k][j + 1]) + 4 * lane + u);
+    }
+    W4 x[kWireRegWords];
+    wreg_unit_words<FAST>(raw, tx.t[k][j], lane, nchars, pad, 5 * j + k, bad, okacc, x);
+#pragma unroll
+    for (int m = 0; m < kWireRegWords; ++m) {
+      const W4 c = canon<BIG>(x[m], f);
+      acc[m] = j == 0 ? c : mod_add(acc[m], c, f);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) raw[u] = next[u];
+  }
+}
+
+// y, r, w -> check w == y r; v, u -> check u == v r.  ok[m]: word m verified
+template <int NP, bool BIG, bool FAST>
+__device__ __forceinline__ void wreg_verify(const TextSet& tx, int n, size_t lane, size_t nchars, uint32_t pad,
+                                            unsigned long long* bad, W4 (&y)[kWireRegWords],
+                                            bool (&ok)[kWireRegWords], const Fp& f) {
+  uint32_t okacc = 0x80808080u;
+  W4 r[kWireRegWords], t[kWireRegWords];
+  wreg_field<NP, BIG, FAST>(tx, 0, n, lane, nchars, pad, bad, okacc, y, f);
+  wreg_field<NP, BIG, FAST>(tx, 1, n, lane, nchars, pad, bad, okacc, r, f);
+  wreg_field<NP, BIG, FAST>(tx, 3, n, lane, nchars, pad, bad, okacc, t, f);  // w
+#pragma unroll
+  for (int m = 0; m < kWireRegWords; ++m) {  // one product at a time (each ~30 live temporaries)
+    ok[m] = eq(mont_mul_v(y[m], r[m], f), t[m]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  W4 v[kWireRegWords];
+  wreg_field<NP, BIG, FAST>(tx, 2, n, lane, nchars, pad, bad, okacc, v, f);
+  wreg_field<NP, BIG, FAST>(tx, 4, n, lane, nchars, pad, bad, okacc, t, f);  // u
+#pragma unroll
+  for (int m = 0; m < kWireRegWords; ++m) {
+    ok[m] = ok[m] & eq(mont_mul_v(v[m], r[m], f), t[m]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (FAST && okacc != 0x80808080u) wreg_find_bad(tx, n, lane, nchars, pad, bad);
+}
+
+// smallest failing word of the wave (lanes own ascending word ranges)
+__device__ __forceinline__ void wreg_report(const bool (&fail)[kWireRegWords], size_t word0,
+                                            unsigned long long* ff) {
+  size_t first = ~(size_t)0;
+#pragma unroll
+  for (int m = kWireRegWords - 1; m >= 0; --m)
+    if (fail[m]) first = word0 + m;
+  report_fail(first != ~(size_t)0, first, ff);
+}
+
+template <int NP, bool BIG, int BS>
+__global__ __launch_bounds__(BS) void k_rv_b64_reg(TextSet tx, int n, size_t words, size_t nchars,
+                                               uint32_t pad, uint4* out_y, unsigned long long* ff,
+                                               unsigned long long* bad, Fp f) {
+  const size_t lane = (size_t)blockIdx.x * BS + threadIdx.x;
+  const size_t word0 = kWireRegWords * lane;
+  if (word0 >= words) return;  // whole lanes past the last word: nothing to read or write
+  const bool fast = ((size_t)blockIdx.x + 1) * BS * 64 + 4 <= nchars;
+  W4 y[kWireRegWords];
+  bool ok[kWireRegWords];
+  if (fast) wreg_verify<NP, BIG, true>(tx, n, lane, nchars, pad, bad, y, ok, f);
+  else wreg_verify<NP, BIG, false>(tx, n, lane, nchars, pad, bad, y, ok, f);
+  bool fail[kWireRegWords];
+#pragma unroll
+  for (int m = 0; m < kWireRegWords; ++m) {
+    const bool in = word0 + m < words;
+    fail[m] = in && !ok[m];
+    if (in) st_out(out_y + word0 + m, redc(y[m], f));
+  }
+  wreg_report(fail, word0, ff);
+}
+
+template <int NP, bool BIG, int BS>
+__global__ __launch_bounds__(BS) void k_mask_b64_reg(TextSet tx, int n, size_t words, size_t nchars,
+                                                 uint32_t pad, const uint4* secrets, size_t n_secrets,
+                                                 uint4* out16, char* out24, unsigned long long* ff,
+                                                 unsigned long long* bad, Fp f) {
+  const size_t lane = (size_t)blockIdx.x * BS + threadIdx.x;
+  const size_t word0 = kWireRegWords * lane;
+  if (word0 >= words) return;
+  uint4 s[kWireRegWords];
+#pragma unroll
+  for (int m = 0; m < kWireRegWords; ++m)
+    s[m] = word0 + m < n_secrets ? ld(secrets + word0 + m) : make_uint4(0, 0, 0, 0);
+  const bool fast = ((size_t)blockIdx.x + 1) * BS * 64 + 4 <= nchars;
+  W4 y[kWireRegWords];
+  bool ok[kWireRegWords];
+  if (fast) wreg_verify<NP, BIG, true>(tx, n, lane, nchars, pad, bad, y, ok, f);
+  else wreg_verify<NP, BIG, false>(tx, n, lane, nchars, pad, bad, y, ok, f);
+  bool fail[kWireRegWords];
+#pragma unroll
+  for (int m = 0; m < kWireRegWords; ++m) {
+    const size_t w = word0 + m;
+    fail[m] = w < words && !ok[m];
+    if (w < n_secrets) {
+      const W4 mk = mod_sub(mont_mul_v(w4(s[m]), r2_word(f), f), y[m], f);
+      if (out16) st_out(out16 + w, mk);
+      if (out24) {  // 24-byte record: three 8-byte stores (lanes 72 B apart)
+        uint32_t g[6];
+        enc_word24(u4(mk), g);
+        uint2* d = reinterpret_cast<uint2*>(out24 + 24 * w);
+        d[0] = make_uint2(g[0], g[1]);
+        d[1] = make_uint2(g[2], g[3]);
+        d[2] = make_uint2(g[4], g[5]);
+      }
+    }
+  }
+  wreg_report(fail, word0, ff);
+}
+
+}  // namespace
+
+// AMPH_WIRE_FORM=lds selects round 2's LDS-transpose form of the two fused
+// wire kernels (A/B); the register form is the default.
+bool wire_reg_form() {
+  static const bool reg = [] {
+    const char* e = std::getenv("AMPH_WIRE_FORM");
+    return !(e && std::string(e) == "lds");
+  }();
+  return reg;
+}
+
+hipError_t launch_rv_b64(const TextSet& tx, int n, size_t words, size_t nchars, uint32_t pad,
+                         uint4* out_y, unsigned long long* ff, unsigned long long* bad, const Fp& f,
+                         const LaunchCfg& c) {
+  if (words == 0) return hipSuccess;
+  if (wire_reg_form()) {
+    constexpr int BS = kWireRegBlock;
+    const size_t lanes = (words + kWireRegWords - 1) / kWireRegWords;
+    const dim3 g((unsigned)((lanes + BS - 1) / BS));
+#define L(NP, BIG) AMPH_LAUNCH((k_rv_b64_reg<NP, BIG, BS>), g, dim3(BS), c, tx, n, words, nchars, pad, out_y, ff, bad, f)
+    if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
+#undef L
+    return hipGetLastError();
+  }
+  constexpr int BS = kWireBlock;
+  const dim3 g((unsigned)((words + Wire<BS>::words - 1) / Wire<BS>::words));
+#define L(NP, BIG) AMPH_LAUNCH((k_rv_b64<NP, BIG, BS>), g, dim3(BS), c, tx, n, words, nchars, pad, out_y, ff, bad, f)
+  if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
+#undef L
+  return hipGetLastError();
+}
+
+hipError_t launch_mask_b64(const TextSet& tx, int n, size_t words, size_t nchars, uint32_t pad,
+                           const uint4* secrets, size_t n_secrets, uint4* out16, char* out24,
+                           unsigned long long* ff, unsigned long long* bad, const Fp& f,
+                           const LaunchCfg& c) {
+  if (words == 0) return hipSuccess;
+  if (wire_reg_form()) {
+    constexpr int BS = kWireRegBlock;
+    const size_t lanes = (words + kWireRegWords - 1) / kWireRegWords;
+    const dim3 g((unsigned)((lanes + BS - 1) / BS));
+#define L(NP, BIG) AMPH_LAUNCH((k_mask_b64_reg<NP, BIG, BS>), g, dim3(BS), c, tx, n, words, nchars, pad, secrets, n_secrets, out16, out24, ff, bad, f)
+    if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
+#undef L
+    return hipGetLastError();
+  }
+  constexpr int BS = kWireBlock;
+  const dim3 g((unsigned)((words + Wire<BS>::words - 1) / Wire<BS>::words));
+#define L(NP, BIG) AMPH_LAUNCH((k_mask_b64<NP, BIG, BS>), g, dim3(BS), c, tx, n, words, nchars, pad, secrets, n_secrets, out16, out24, ff, bad, f)
+  if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
+#undef L
+  return hipGetLastError();
+}
+
+}  // namespace amph

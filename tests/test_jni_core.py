@@ -33,6 +33,10 @@ IAE = "java/lang/IllegalArgumentException"
 @pytest.fixture(scope="module")
 def J():
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "jni"), "mock"], check=True)
+    # amphora_amd first: it loads torch's HIP runtime before libamphora_hip, so
+    # the mock's libamphora_hip binds to that one instance (a process whose first
+    # HIP library is /opt/rocm's sees no device through torch's, and vice versa)
+    import amphora_amd  # noqa: F401
     L = C.CDLL(MOCK)
     vp = C.c_void_p
     L.mock_env.restype = vp

@@ -15,8 +15,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HERE = os.path.join(ROOT, "amphora_amd")
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libamphora_hip.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("kernels.hip", "codec.hip", "exchange.hip", "capi.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("field.hpp", "kernels.hpp", "host_stream.hpp")] + [
+SOURCES = [os.path.join(CSRC, f) for f in ("kernels.hip", "wire.hip", "codec.hip", "exchange.hip", "capi.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("field.hpp", "kernels.hpp", "host_stream.hpp", "devio.hpp",
+                                                   "b64.hpp", "decimal.hpp")] + [
     os.path.join(ROOT, "include", "amphora.h")]
 ARCH = os.environ.get("AMPH_OFFLOAD_ARCH", "gfx950")
 
@@ -35,19 +36,51 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
-        return LIB
-    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-mcode-object-version=5", "-Wall", "-I" + os.path.join(ROOT, "include"),
-           "-Wl,-rpath,/opt/rocm/lib", "-o", LIB + ".tmp"] + SOURCES
-    if verbose:
-        print(" ".join(cmd))
+def compile_link(out: str, flags, link_flags, objdir: str, verbose: bool = False) -> None:
+    """Every translation unit compiled by its own hipcc process at once (the
+    fused wire kernels' unit alone takes minutes), then one link.  A unit is
+    recompiled when it or a shared header is newer than its object."""
+    os.makedirs(objdir, exist_ok=True)
+    hdrs = [d for d in DEPS if d not in SOURCES]
+    procs = []
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if os.path.exists(obj) and all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in hdrs + [src]):
+            continue
+        cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-std=c++17", "-fPIC", "-mcode-object-version=5",
+               "-I" + os.path.join(ROOT, "include"), "-c", src, "-o", obj + ".tmp"] + list(flags)
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((obj, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
+    failed = []
+    for obj, p in procs:
+        out_text, _ = p.communicate()
+        if p.returncode != 0:
+            failed.append(obj)
+            sys.stderr.write(out_text)
+        else:
+            os.replace(obj + ".tmp", obj)
+    if failed:
+        raise RuntimeError("hipcc failed: %s" % ", ".join(os.path.basename(f) for f in failed))
+    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-shared", "-fPIC", "-Wl,-rpath,/opt/rocm/lib", "-o",
+           out + ".tmp"] + objs + list(link_flags)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
-        raise RuntimeError("hipcc failed building libamphora_hip.so")
-    os.replace(LIB + ".tmp", LIB)
+        raise RuntimeError("link failed: %s" % out)
+    os.replace(out + ".tmp", out)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return LIB
+    objdir = os.path.join(ROOT, "build", "obj")
+    if force:
+        for f in os.listdir(objdir) if os.path.isdir(objdir) else []:
+            os.remove(os.path.join(objdir, f))
+    compile_link(LIB, ["-O3", "-Wall", "-Wno-pass-failed"], [], objdir, verbose)
     return LIB
 
 
@@ -104,11 +137,10 @@ def build_sanitized(force: bool = False) -> dict:
     mirror = os.path.join(SAN_DIR, "mirror_test")
     orc = os.path.join(SAN_DIR, "oracle_sanitize")
     orc_src = os.path.join(ROOT, "tests", "cpp", "oracle_sanitize.c")
+    if force or not os.path.exists(lib) or any(os.path.getmtime(d) > os.path.getmtime(lib) for d in DEPS):
+        san = [x for f in SAN_FLAGS for x in ("-Xarch_host", f)]
+        compile_link(lib, ["-O1", "-g"] + san, san, os.path.join(SAN_DIR, "obj"))
     jobs = [
-        (lib, DEPS, [hipcc(), "--offload-arch=%s" % ARCH, "-O1", "-g", "-std=c++17", "-fPIC", "-shared",
-                     "-mcode-object-version=5", "-I" + os.path.join(ROOT, "include"),
-                     "-Wl,-rpath,/opt/rocm/lib", "-o", lib] + SOURCES
-         + [x for f in SAN_FLAGS for x in ("-Xarch_host", f)]),
         (mirror, [CPP_TEST_SRC, os.path.join(ROOT, "include", "amphora.hpp"), lib],
          ["/opt/rocm/llvm/bin/clang++", "-std=c++17", "-O1", "-g", "-I" + os.path.join(ROOT, "include"),
           CPP_TEST_SRC, "-L" + SAN_DIR, "-lamphora_hip", "-Wl,-rpath,$ORIGIN", "-o", mirror] + SAN_FLAGS),

@@ -29,17 +29,26 @@ pmc() {  # pmc NAME COUNTERS... -- CMD...
   return $rc
 }
 run_all() {
-  [ -n "$SKIP_TESTS" ] || step pytest 600 python3 -u -m pytest ${PYTEST_FILES:-tests/test_jni_core.py} -m gpu -x -v --timeout 300 --timeout-method thread || return
+  [ -n "$SKIP_TESTS" ] || step pytest 600 python3 -u -m pytest ${PYTEST_FILES:-tests/test_wire_fused.py tests/test_wire.py tests/test_jni_core.py} -m gpu -x -v --timeout 300 --timeout-method thread || return
   [ -n "$SKIP_TRACE" ] || { (cd /tmp && export TMPDIR=/tmp && timeout -k 10 120 rocprofv3 --hip-trace --stats -d "$OUT/hiptrace_new" -o t --output-format csv -- "$ROOT/tools/multi_latency" "$ROOT/amphora_amd/libamphora_hip.so" 1024 100 0,0,0) > "$OUT/hiptrace_new.log" 2>&1 && echo "hiptrace_new ok" >> "$OUT/status.txt" || return; }
   [ -n "$SKIP_TRACE" ] || { (cd /tmp && export TMPDIR=/tmp && timeout -k 10 120 rocprofv3 --hip-trace --stats -d "$OUT/hiptrace_old" -o t --output-format csv -- "$ROOT/tools/multi_latency" "$ROOT/build/prev/libamphora_hip_r3.so" 1024 100 0,0,0) > "$OUT/hiptrace_old.log" 2>&1 && echo "hiptrace_old ok" >> "$OUT/status.txt" || return; }
-  step wire 300 python3 tools/wire_kernels.py || return
+  for form in reg lds; do
+    ( export AMPH_WIRE_FORM=$form; step wire_$form 300 python3 tools/wire_kernels.py ) || return
+  done
+  ( export AMPH_WIRE_FORM=reg; step wire_reg2 300 python3 tools/wire_kernels.py ) || return
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/wire_ktrace" -o k --output-format csv -- python3 "$ROOT/tools/wire_kernels.py") > "$OUT/wire_ktrace.log" 2>&1 && echo "wire_ktrace ok" >> "$OUT/status.txt" || return
   [ -n "$SKIP_PMC" ] && return 0
-  pmc pmc0 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_WAVES -- python3 "$ROOT/tools/wire_kernels.py" --reps 3 || return
-  pmc pmc1 FETCH_SIZE -- python3 "$ROOT/tools/wire_kernels.py" --reps 3 || return
-  pmc pmc2 WRITE_SIZE -- python3 "$ROOT/tools/wire_kernels.py" --reps 3 || return
+  for form in lds reg; do
+    ( export AMPH_WIRE_FORM=$form
+      pmc pmc0_$form SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_WAVES -- python3 "$ROOT/tools/wire_kernels.py" --reps 3 &&
+      pmc pmc1_$form FETCH_SIZE -- python3 "$ROOT/tools/wire_kernels.py" --reps 3 &&
+      pmc pmc2_$form WRITE_SIZE -- python3 "$ROOT/tools/wire_kernels.py" --reps 3 ) || return
+  done
   (timeout -k 10 60 rocprofv3 -L > "$OUT/counters.txt" 2>&1; true)
-  pmc pmc3 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR -- python3 "$ROOT/tools/wire_kernels.py" --reps 3 || return
+  for form in lds reg; do
+    ( export AMPH_WIRE_FORM=$form
+      pmc pmc3_$form SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR -- python3 "$ROOT/tools/wire_kernels.py" --reps 3 ) || return
+  done
 }
 run_all
 rc=$?
