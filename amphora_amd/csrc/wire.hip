@@ -288,7 +288,7 @@ __device__ __forceinline__ void wreg_unit_words(const uint4 (&raw)[4], const cha
 
 // a lane whose characters were not all valid (okacc): the first bad offset
 // of every field, re-read one unit at a time (rare: a malformed response)
-__device__ __noinline__ void wreg_find_bad(const TextSet& tx, int n, size_t lane, size_t nchars, uint32_t pad,
+__device__ __forceinline__ void wreg_find_bad(const TextSet& tx, int n, size_t lane, size_t nchars, uint32_t pad,
                                            unsigned long long* bad) {
   for (int j = 0; j < n; ++j)
     for (int k = 0; k < 5; ++k)
@@ -432,6 +432,7 @@ __global__ __launch_bounds__(BS) void k_mask_b64_reg(TextSet tx, int n, size_t w
 
 }  // namespace
 
+#ifndef AMPH_WIRE_KERNELS_ONLY  // (tools/ubench: the kernels without the launchers' instantiations)
 // AMPH_WIRE_FORM=lds selects round 2's LDS-transpose form of the two fused
 // wire kernels (A/B); the register form is the default.
 bool wire_reg_form() {
@@ -484,5 +485,7 @@ hipError_t launch_mask_b64(const TextSet& tx, int n, size_t words, size_t nchars
 #undef L
   return hipGetLastError();
 }
+
+#endif  // AMPH_WIRE_KERNELS_ONLY
 
 }  // namespace amph

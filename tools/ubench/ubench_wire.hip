@@ -2,6 +2,7 @@
 // (kernels.hip) at 1 Mi words x 2 parties and 4 Mi x 3, outputs compared
 // across sizes; the texts are made on the GPU with the product base64 encoder.
 #include "../../amphora_amd/csrc/kernels.hip"
+#include "../../amphora_amd/csrc/wire.hip"
 #include <algorithm>
 #include <cstdio>
 #include <vector>
