@@ -103,26 +103,6 @@ __device__ __forceinline__ uint32_t dec_unit16(const uint4 v, uint32_t (&o)[3]) 
   return firstbad;
 }
 
-// The same decode without the offset search: the validity bits of the 16
-// characters are ANDed into okacc (stays 0x80808080 while every character
-// is in the alphabet), so a caller that decodes many units keeps one
-// branch-free accumulator and locates a bad character only if one exists.
-__device__ __forceinline__ void dec_unit16_acc(const uint4 v, uint32_t (&o)[3], uint32_t& okacc) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint32_t g[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    uint32_t val;
-    const uint32_t x = dec4_values(w[q], val);
-    okacc &= val;
-    g[q] = (__builtin_amdgcn_udot4(x, 0x00000140u, 0u, false) << 12) |
-           __builtin_amdgcn_udot4(x, 0x01400000u, 0u, false);
-  }
-  o[0] = __builtin_amdgcn_perm(g[1], g[0], 0x06000102u);
-  o[1] = __builtin_amdgcn_perm(g[2], g[1], 0x05060001u);
-  o[2] = __builtin_amdgcn_perm(g[3], g[2], 0x04050600u);
-}
-
 // A 16-byte word -> its 24-character record (5 full groups, then 1 byte and
 // "=="), as 6 little-endian dwords.
 __device__ __forceinline__ void enc_word24(const uint4 v, uint32_t (&g)[6]) {

@@ -1,9 +1,10 @@
 // The fused wire-format kernels: K_RV / K_MASK straight from the base64 text
 // of the ODO fields (getSecret / createSecret with Jackson's base64 decode of
-// every byte[] field, DefaultAmphoraClient.java:150-170,206-217), in two
-// forms -- round 2's LDS-transpose form and round 4's register form (the
-// default; AMPH_WIRE_FORM=lds for A/B).  Roofline: HBM (text + secrets +
-// outputs), see DESIGN.md §4a.
+// every byte[] field, DefaultAmphoraClient.java:150-170,206-217): the text is
+// decoded in the workgroup and consumed through LDS.  Bound: the decode's
+// integer VALU work ("Wire kernels, round 4": a register form
+// without LDS, a persistent software-pipelined form and an occupancy sweep
+// were measured and rejected -- tools/ubench/ubench_wire_occ.hip).
 #include <cstdlib>
 #include <string>
 
@@ -85,10 +86,10 @@ template <int NP, bool BIG, bool FAST, int BS>
 __device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nchars, uint32_t pad,
                                             size_t words, uint4 (&raw)[5][NP > 0 ? NP : 1],
                                             uint32_t (*lds)[3 * BS], W4 (&acc)[5],
-                                            unsigned long long* bad, const Fp& f) {
+                                            unsigned long long* bad, const Fp& f, size_t tile) {
   constexpr int G = WireGroups<NP>::G, NB = WireGroups<NP>::bufs;
-  const size_t unit = (size_t)blockIdx.x * BS + threadIdx.x;
-  const size_t word = (size_t)blockIdx.x * Wire<BS>::words + threadIdx.x;
+  const size_t unit = tile * BS + threadIdx.x;
+  const size_t word = tile * Wire<BS>::words + threadIdx.x;
   const bool consumer = threadIdx.x < Wire<BS>::words && word < words;
   const int np = NP > 0 ? NP : n;
   int slot = 0;  // LDS buffer of the next field
@@ -141,15 +142,59 @@ __device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nch
 }
 
 template <int NP, int BS>
-__device__ __forceinline__ void wire_load(const TextSet& tx, uint4 (&raw)[5][NP > 0 ? NP : 1]) {
+__device__ __forceinline__ void wire_load(const TextSet& tx, uint4 (&raw)[5][NP > 0 ? NP : 1], size_t tile) {
   if constexpr (NP > 0) {
-    const size_t unit = (size_t)blockIdx.x * BS + threadIdx.x;
+    const size_t unit = tile * BS + threadIdx.x;
 #pragma unroll
     for (int k = 0; k < 5; ++k)
 #pragma unroll
       for (int j = 0; j < NP; ++j)
         if (kWirePrefetch == 0 || k * NP + j < kWirePrefetch)
           raw[k][j] = ld(reinterpret_cast<const uint4*>(tx.t[k][j]) + unit);
+  }
+}
+
+// K_MASK from the wire, after a tile's fields are summed: verify, mask the
+// secret, and write the masked word and / or its 24-character record (records
+// staged through LDS -- the decode buffers -- and stored as 16-byte runs).
+template <int NP, int BS>
+__device__ __forceinline__ void mask_tile_out(size_t tile, size_t words, const uint4 s, size_t n_secrets,
+                                              W4 (&acc)[5], uint4* out16, char* out24,
+                                              unsigned long long* ff, uint32_t (*lds)[3 * BS], const Fp& f) {
+  constexpr int WW = Wire<BS>::words;
+  const size_t word = tile * WW + threadIdx.x;
+  const bool has_secret = threadIdx.x < WW && word < n_secrets;
+  uint32_t g[6];
+  if (threadIdx.x < WW) {
+    const bool in = word < words;
+    bool ok = true;
+    if (in) ok = (int)eq(mont_mul_v(acc[0], acc[1], f), acc[3]) & (int)eq(mont_mul_v(acc[2], acc[1], f), acc[4]);
+    report_fail(in && !ok, word, ff);
+    if (has_secret) {
+      const uint4 m = u4(mod_sub(mont_mul_v(w4(s), r2_word(f), f), acc[0], f));
+      if (out16) st_out(out16 + word, w4(m));
+      enc_word24(m, g);
+    }
+  }
+  if (!out24) return;
+  // records: 24 B per word through LDS (the two decode buffers, 24 KiB), then
+  // the workgroup's run as 16-byte stores (full workgroups; the last one's
+  // tail per byte)
+  __syncthreads();
+  uint32_t* l = &lds[0][0];
+  if (has_secret)
+#pragma unroll
+    for (int q = 0; q < 6; ++q) l[6 * threadIdx.x + q] = g[q];
+  __syncthreads();
+  const size_t w0 = tile * WW;
+  const size_t nrec = w0 < n_secrets ? min((size_t)WW, n_secrets - w0) : 0;
+  char* dst = out24 + 24 * w0;
+  if (nrec == (size_t)WW) {
+    for (int q = threadIdx.x; q < 6 * WW / 4; q += BS)
+      reinterpret_cast<uint4*>(dst)[q] = make_uint4(l[4 * q], l[4 * q + 1], l[4 * q + 2], l[4 * q + 3]);
+  } else {
+    for (size_t q = threadIdx.x; q < 6 * nrec; q += BS)
+      reinterpret_cast<uint32_t*>(dst)[q] = l[q];
   }
 }
 
@@ -166,10 +211,10 @@ __global__ __launch_bounds__(BS) void k_rv_b64(TextSet tx, int n, size_t words, 
   uint4 raw[5][NP > 0 ? NP : 1];
   const bool fast = ((size_t)blockIdx.x + 1) * Wire<BS>::chars + 4 <= nchars;
   if (fast) {
-    wire_load<NP, BS>(tx, raw);
-    wire_fields<NP, BIG, true, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f);
+    wire_load<NP, BS>(tx, raw, blockIdx.x);
+    wire_fields<NP, BIG, true, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x);
   } else {
-    wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f);
+    wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x);
   }
   const size_t word = (size_t)blockIdx.x * Wire<BS>::words + threadIdx.x;
   if (threadIdx.x < Wire<BS>::words) {  // whole waves
@@ -203,259 +248,22 @@ __global__ __launch_bounds__(BS) void k_mask_b64(TextSet tx, int n, size_t words
   if (has_secret) s = ld(secrets + word);
   const bool fast = ((size_t)blockIdx.x + 1) * Wire<BS>::chars + 4 <= nchars;
   if (fast) {
-    wire_load<NP, BS>(tx, raw);
-    wire_fields<NP, BIG, true, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f);
+    wire_load<NP, BS>(tx, raw, blockIdx.x);
+    wire_fields<NP, BIG, true, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x);
   } else {
-    wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f);
+    wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x);
   }
-  uint32_t g[6];
-  if (threadIdx.x < WW) {
-    const bool in = word < words;
-    bool ok = true;
-    if (in) ok = (int)eq(mont_mul_v(acc[0], acc[1], f), acc[3]) & (int)eq(mont_mul_v(acc[2], acc[1], f), acc[4]);
-    report_fail(in && !ok, word, ff);
-    if (has_secret) {
-      const uint4 m = u4(mod_sub(mont_mul_v(w4(s), r2_word(f), f), acc[0], f));
-      if (out16) st_out(out16 + word, w4(m));
-      enc_word24(m, g);
-    }
-  }
-  if (!out24) return;
-  // records: 24 B per word through LDS (the two decode buffers, 24 KiB), then
-  // the workgroup's run as 16-byte stores (full workgroups; the last one's
-  // tail per byte)
-  __syncthreads();
-  uint32_t* l = &lds[0][0];
-  if (has_secret)
-#pragma unroll
-    for (int q = 0; q < 6; ++q) l[6 * threadIdx.x + q] = g[q];
-  __syncthreads();
-  const size_t w0 = (size_t)blockIdx.x * WW;
-  const size_t nrec = w0 < n_secrets ? min((size_t)WW, n_secrets - w0) : 0;
-  char* dst = out24 + 24 * w0;
-  if (nrec == (size_t)WW) {
-    for (int q = threadIdx.x; q < 6 * WW / 4; q += BS)
-      reinterpret_cast<uint4*>(dst)[q] = make_uint4(l[4 * q], l[4 * q + 1], l[4 * q + 2], l[4 * q + 3]);
-  } else {
-    for (size_t q = threadIdx.x; q < 6 * nrec; q += BS)
-      reinterpret_cast<uint32_t*>(dst)[q] = l[q];
-  }
+  mask_tile_out<NP, BS>(blockIdx.x, words, s, n_secrets, acc, out16, out24, ff, lds, f);
 }
 
-// ---- register form of the fused wire kernels (no LDS, no barrier) --------------
-// 64 characters of a field are exactly 48 bytes = 3 words, so a lane that owns
-// THREE consecutive words reads its 64 characters (four 16-byte loads, lanes
-// 64 B apart) and has every byte of its words in its own registers after the
-// decode: no LDS transpose, no barrier, every wave independent of the others.
-// Fields are consumed in the order y, r, w, v, u so that w is checked against
-// y r and dropped before v and u are summed (48 live accumulator registers
-// instead of 60); one field's four loads are issued before the previous
-// field's decode.
-constexpr int kWireRegBlock = 256;
-constexpr int kWireRegWords = 3;  // words per lane
-
-// one party's field: this lane's 64 characters (units 4 lane .. 4 lane + 3)
-// -> its three words.  FAST: full units, validity ANDed into okacc (the
-// offset of a bad character is searched for afterwards, wreg_find_bad);
-// otherwise per character (padding, the text's end) with the offset reported
-// at once.
-template <bool FAST>
-__device__ __forceinline__ void wreg_unit_words(const uint4 (&raw)[4], const char* t, size_t lane,
-                                                size_t nchars, uint32_t pad, int fieldno,
-                                                unsigned long long* bad, uint32_t& okacc,
-                                                W4 (&x)[kWireRegWords]) {
-  uint32_t o[12];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    uint32_t q[3];
-    if constexpr (FAST) {
-      dec_unit16_acc(raw[u], q, okacc);
-      // one unit at a time: interleaving the four units' 16 independent group
-      // decodes costs ~100 VGPRs for little VALU latency to hide
-      __builtin_amdgcn_sched_barrier(0);
-    } else {
-      const size_t unit = 4 * lane + u;
-      const uint32_t fb = dec_unit_slow(t, unit, nchars, pad, q);
-      if (fb != 0xFFFFFFFFu) atomicMin(bad, (unsigned long long)((size_t)fieldno * nchars + 16 * unit + fb));
-    }
-    o[3 * u] = q[0];
-    o[3 * u + 1] = q[1];
-    o[3 * u + 2] = q[2];
-  }
-#pragma unroll
-  for (int m = 0; m < kWireRegWords; ++m) x[m] = W4{{o[4 * m], o[4 * m + 1], o[4 * m + 2], o[4 * m + 3]}};
-}
-
-// a lane whose characters were not all valid (okacc): the first bad offset
-// of every field, re-read one unit at a time (rare: a malformed response)
-__device__ __forceinline__ void wreg_find_bad(const TextSet& tx, int n, size_t lane, size_t nchars, uint32_t pad,
-                                           unsigned long long* bad) {
-  for (int j = 0; j < n; ++j)
-    for (int k = 0; k < 5; ++k)
-      for (int u = 0; u < 4; ++u) {
-        uint32_t q[3];
-        const size_t unit = 4 * lane + u;
-        const uint32_t fb = dec_unit_slow(tx.t[k][j], unit, nchars, pad, q);
-        if (fb != 0xFFFFFFFFu) atomicMin(bad, (unsigned long long)((size_t)(5 * j + k) * nchars + 16 * unit + fb));
-      }
-}
-
-template <int NP, bool BIG, bool FAST>
-__device__ __forceinline__ void wreg_field(const TextSet& tx, int k, int n, size_t lane, size_t nchars,
-                                           uint32_t pad, unsigned long long* bad, uint32_t& okacc,
-                                           W4 (&acc)[kWireRegWords], const Fp& f) {
-  // A runtime loop over the parties (not unrolled): the compiler then cannot
-  // interleave several parties' or fields' decodes, which took every lane to
-  // 256 VGPRs (one wave per SIMD) when the whole verify was unrolled.  The
-  // next party's four loads are issued before this party's decode.
-  const int np = NP > 0 ? NP : n;
-  uint4 raw[4] = {};
-  if constexpr (FAST) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) raw[u] = ld(reinterpret_cast<const uint4*>(tx.t[k][0]) + 4 * lane + u);
-  }
-#pragma unroll 1
-  for (int j = 0; j < np; ++j) {
-    uint4 next[4] = {};
-    if constexpr (FAST) {
-      if (j + 1 < np)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) next[u] = ld(reinterpret_cast<const uint4*>(tx.t[k][j + 1]) + 4 * lane + u);
-    }
-    W4 x[kWireRegWords];
-    wreg_unit_words<FAST>(raw, tx.t[k][j], lane, nchars, pad, 5 * j + k, bad, okacc, x);
-#pragma unroll
-    for (int m = 0; m < kWireRegWords; ++m) {
-      const W4 c = canon<BIG>(x[m], f);
-      acc[m] = j == 0 ? c : mod_add(acc[m], c, f);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) raw[u] = next[u];
-  }
-}
-
-// y, r, w -> check w == y r; v, u -> check u == v r.  ok[m]: word m verified
-template <int NP, bool BIG, bool FAST>
-__device__ __forceinline__ void wreg_verify(const TextSet& tx, int n, size_t lane, size_t nchars, uint32_t pad,
-                                            unsigned long long* bad, W4 (&y)[kWireRegWords],
-                                            bool (&ok)[kWireRegWords], const Fp& f) {
-  uint32_t okacc = 0x80808080u;
-  W4 r[kWireRegWords], t[kWireRegWords];
-  wreg_field<NP, BIG, FAST>(tx, 0, n, lane, nchars, pad, bad, okacc, y, f);
-  wreg_field<NP, BIG, FAST>(tx, 1, n, lane, nchars, pad, bad, okacc, r, f);
-  wreg_field<NP, BIG, FAST>(tx, 3, n, lane, nchars, pad, bad, okacc, t, f);  // w
-#pragma unroll
-  for (int m = 0; m < kWireRegWords; ++m) {  // one product at a time (each ~30 live temporaries)
-    ok[m] = eq(mont_mul_v(y[m], r[m], f), t[m]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  W4 v[kWireRegWords];
-  wreg_field<NP, BIG, FAST>(tx, 2, n, lane, nchars, pad, bad, okacc, v, f);
-  wreg_field<NP, BIG, FAST>(tx, 4, n, lane, nchars, pad, bad, okacc, t, f);  // u
-#pragma unroll
-  for (int m = 0; m < kWireRegWords; ++m) {
-    ok[m] = ok[m] & eq(mont_mul_v(v[m], r[m], f), t[m]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if (FAST && okacc != 0x80808080u) wreg_find_bad(tx, n, lane, nchars, pad, bad);
-}
-
-// smallest failing word of the wave (lanes own ascending word ranges)
-__device__ __forceinline__ void wreg_report(const bool (&fail)[kWireRegWords], size_t word0,
-                                            unsigned long long* ff) {
-  size_t first = ~(size_t)0;
-#pragma unroll
-  for (int m = kWireRegWords - 1; m >= 0; --m)
-    if (fail[m]) first = word0 + m;
-  report_fail(first != ~(size_t)0, first, ff);
-}
-
-template <int NP, bool BIG, int BS>
-__global__ __launch_bounds__(BS) void k_rv_b64_reg(TextSet tx, int n, size_t words, size_t nchars,
-                                               uint32_t pad, uint4* out_y, unsigned long long* ff,
-                                               unsigned long long* bad, Fp f) {
-  const size_t lane = (size_t)blockIdx.x * BS + threadIdx.x;
-  const size_t word0 = kWireRegWords * lane;
-  if (word0 >= words) return;  // whole lanes past the last word: nothing to read or write
-  const bool fast = ((size_t)blockIdx.x + 1) * BS * 64 + 4 <= nchars;
-  W4 y[kWireRegWords];
-  bool ok[kWireRegWords];
-  if (fast) wreg_verify<NP, BIG, true>(tx, n, lane, nchars, pad, bad, y, ok, f);
-  else wreg_verify<NP, BIG, false>(tx, n, lane, nchars, pad, bad, y, ok, f);
-  bool fail[kWireRegWords];
-#pragma unroll
-  for (int m = 0; m < kWireRegWords; ++m) {
-    const bool in = word0 + m < words;
-    fail[m] = in && !ok[m];
-    if (in) st_out(out_y + word0 + m, redc(y[m], f));
-  }
-  wreg_report(fail, word0, ff);
-}
-
-template <int NP, bool BIG, int BS>
-__global__ __launch_bounds__(BS) void k_mask_b64_reg(TextSet tx, int n, size_t words, size_t nchars,
-                                                 uint32_t pad, const uint4* secrets, size_t n_secrets,
-                                                 uint4* out16, char* out24, unsigned long long* ff,
-                                                 unsigned long long* bad, Fp f) {
-  const size_t lane = (size_t)blockIdx.x * BS + threadIdx.x;
-  const size_t word0 = kWireRegWords * lane;
-  if (word0 >= words) return;
-  uint4 s[kWireRegWords];
-#pragma unroll
-  for (int m = 0; m < kWireRegWords; ++m)
-    s[m] = word0 + m < n_secrets ? ld(secrets + word0 + m) : make_uint4(0, 0, 0, 0);
-  const bool fast = ((size_t)blockIdx.x + 1) * BS * 64 + 4 <= nchars;
-  W4 y[kWireRegWords];
-  bool ok[kWireRegWords];
-  if (fast) wreg_verify<NP, BIG, true>(tx, n, lane, nchars, pad, bad, y, ok, f);
-  else wreg_verify<NP, BIG, false>(tx, n, lane, nchars, pad, bad, y, ok, f);
-  bool fail[kWireRegWords];
-#pragma unroll
-  for (int m = 0; m < kWireRegWords; ++m) {
-    const size_t w = word0 + m;
-    fail[m] = w < words && !ok[m];
-    if (w < n_secrets) {
-      const W4 mk = mod_sub(mont_mul_v(w4(s[m]), r2_word(f), f), y[m], f);
-      if (out16) st_out(out16 + w, mk);
-      if (out24) {  // 24-byte record: three 8-byte stores (lanes 72 B apart)
-        uint32_t g[6];
-        enc_word24(u4(mk), g);
-        uint2* d = reinterpret_cast<uint2*>(out24 + 24 * w);
-        d[0] = make_uint2(g[0], g[1]);
-        d[1] = make_uint2(g[2], g[3]);
-        d[2] = make_uint2(g[4], g[5]);
-      }
-    }
-  }
-  wreg_report(fail, word0, ff);
-}
 
 }  // namespace
 
 #ifndef AMPH_WIRE_KERNELS_ONLY  // (tools/ubench: the kernels without the launchers' instantiations)
-// AMPH_WIRE_FORM=lds selects round 2's LDS-transpose form of the two fused
-// wire kernels (A/B); the register form is the default.
-bool wire_reg_form() {
-  static const bool reg = [] {
-    const char* e = std::getenv("AMPH_WIRE_FORM");
-    return !(e && std::string(e) == "lds");
-  }();
-  return reg;
-}
-
 hipError_t launch_rv_b64(const TextSet& tx, int n, size_t words, size_t nchars, uint32_t pad,
                          uint4* out_y, unsigned long long* ff, unsigned long long* bad, const Fp& f,
                          const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
-  if (wire_reg_form()) {
-    constexpr int BS = kWireRegBlock;
-    const size_t lanes = (words + kWireRegWords - 1) / kWireRegWords;
-    const dim3 g((unsigned)((lanes + BS - 1) / BS));
-#define L(NP, BIG) AMPH_LAUNCH((k_rv_b64_reg<NP, BIG, BS>), g, dim3(BS), c, tx, n, words, nchars, pad, out_y, ff, bad, f)
-    if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
-#undef L
-    return hipGetLastError();
-  }
   constexpr int BS = kWireBlock;
   const dim3 g((unsigned)((words + Wire<BS>::words - 1) / Wire<BS>::words));
 #define L(NP, BIG) AMPH_LAUNCH((k_rv_b64<NP, BIG, BS>), g, dim3(BS), c, tx, n, words, nchars, pad, out_y, ff, bad, f)
@@ -469,15 +277,6 @@ hipError_t launch_mask_b64(const TextSet& tx, int n, size_t words, size_t nchars
                            unsigned long long* ff, unsigned long long* bad, const Fp& f,
                            const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
-  if (wire_reg_form()) {
-    constexpr int BS = kWireRegBlock;
-    const size_t lanes = (words + kWireRegWords - 1) / kWireRegWords;
-    const dim3 g((unsigned)((lanes + BS - 1) / BS));
-#define L(NP, BIG) AMPH_LAUNCH((k_mask_b64_reg<NP, BIG, BS>), g, dim3(BS), c, tx, n, words, nchars, pad, secrets, n_secrets, out16, out24, ff, bad, f)
-    if (f.big) { AMPH_DISPATCH_NP(n, true, L) } else { AMPH_DISPATCH_NP(n, false, L) }
-#undef L
-    return hipGetLastError();
-  }
   constexpr int BS = kWireBlock;
   const dim3 g((unsigned)((words + Wire<BS>::words - 1) / Wire<BS>::words));
 #define L(NP, BIG) AMPH_LAUNCH((k_mask_b64<NP, BIG, BS>), g, dim3(BS), c, tx, n, words, nchars, pad, secrets, n_secrets, out16, out24, ff, bad, f)
