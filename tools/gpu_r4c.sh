@@ -35,6 +35,7 @@ run_all() {
   prof bench_write 300 --kernel-trace --pmc WRITE_SIZE -d "$OUT/bench_write" -o pmc --output-format csv -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline || return
   step jni_regions 300 python3 tools/bench_jni_regions.py || return
   step wire 300 python3 tools/wire_kernels.py || return
+  step valu_rate 120 ./tools/ubench/ubench_valu_rate || return
 }
 run_all
 rc=$?
