@@ -36,6 +36,9 @@ run_all() {
   step jni_regions 300 python3 tools/bench_jni_regions.py || return
   step wire 300 python3 tools/wire_kernels.py || return
   step valu_rate 120 ./tools/ubench/ubench_valu_rate || return
+  for blk in 256 512 1024 256 512 1024; do
+    ( export AMPH_BLOCK=$blk; step bench_blk${blk}_$RANDOM 300 python3 bench.py --no-cpu-baseline --steps 200 --warmup 20 ) || return
+  done
 }
 run_all
 rc=$?
