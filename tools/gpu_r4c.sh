@@ -36,6 +36,8 @@ run_all() {
   step jni_regions 300 python3 tools/bench_jni_regions.py || return
   step wire 300 python3 tools/wire_kernels.py || return
   step valu_rate 120 ./tools/ubench/ubench_valu_rate || return
+  timeout -k 10 120 ./tools/ubench/wocc/u_g5p0 4194304 20 probe >> "$OUT/wire_probe.jsonl" 2>> "$OUT/wire_probe.err" || return
+  timeout -k 10 200 ./tools/ubench/wocc/u_g5p0 16777216 5 probe >> "$OUT/wire_probe.jsonl" 2>> "$OUT/wire_probe.err" || return
   for blk in 256 512 1024 256 512 1024; do
     ( export AMPH_BLOCK=$blk; step bench_blk${blk}_$RANDOM 300 python3 bench.py --no-cpu-baseline --steps 200 --warmup 20 ) || return
   done
