@@ -655,8 +655,10 @@ class Context:
         import torch
         if buf is None:
             buf = torch.empty((5, n, words, 16), dtype=torch.uint8, device="cuda:%d" % self.device)
-        elif tuple(buf.shape) != (5, n, words, 16) or buf.dtype != torch.uint8 or not buf.is_contiguous():
-            raise ValueError("buf must be a contiguous (5, n, words, 16) uint8 device tensor")
+        elif (tuple(buf.shape[:2]) != (5, n) or buf.shape[2] < words or tuple(buf.shape[3:]) != (16,)
+              or buf.dtype != torch.uint8 or not buf.is_contiguous()):
+            raise ValueError("buf must be a contiguous (5, n, >= words, 16) uint8 device tensor")
+        buf = buf[:, :, :words]  # a padded slab: each field starts at its own row of the slab
         plain = torch.empty((words, 16), dtype=torch.uint8, device=buf.device) if with_plain else None
         ptrs = (C.c_void_p * (5 * n))(*[buf[k, j].data_ptr() for k in range(5) for j in range(n)])
         stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)

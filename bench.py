@@ -165,6 +165,9 @@ def parse():
     ap.add_argument("--no-scatter-gather", action="store_true",
                     help="skip the root-held (RCCL scatter/gather-inclusive) C4 measurement that "
                          "follows the device-resident one when a process group exists")
+    ap.add_argument("--pad-words", type=int, default=0,
+                    help="device mode: allocate each party's five ODO fields as rows of a slab "
+                         "W + PAD words long (PAD = 0: rows exactly 2^k words apart)")
     ap.add_argument("--sg-steps", type=int, default=3)
     ap.add_argument("--sg-warmup", type=int, default=1)
     a = ap.parse_args()
@@ -593,8 +596,10 @@ def main():
     else:  # C2 / C3 / custom: W words on every rank
         start, W = rank * a.words, a.words
         total_words = a.words * world
-    mask_odos, mbuf, mplain = ctx.synth_odos(seed=1000 + rank, n=n, words=W, with_plain=True)
-    share_odos, sbuf, splain = ctx.synth_odos(seed=2000 + rank, n=n, words=W, with_plain=True)
+    slab = (lambda: torch.empty((5, n, W + a.pad_words, 16), dtype=torch.uint8, device="cuda")) \
+        if a.pad_words else (lambda: None)
+    mask_odos, mbuf, mplain = ctx.synth_odos(seed=1000 + rank, n=n, words=W, with_plain=True, buf=slab())
+    share_odos, sbuf, splain = ctx.synth_odos(seed=2000 + rank, n=n, words=W, with_plain=True, buf=slab())
     secrets = ctx.synth_words(seed=3000 + rank, count=W)
     torch.cuda.synchronize()
 
@@ -726,6 +731,8 @@ def main():
             "scaling": a.scaling, "vs_baseline": None, "dtype": "u128 mod-p (4x u32 limbs)",
             "data": "synthetic: device-generated honest %d-party ODOs + secrets (seeded)" % n,
             "config": workload_config(a, world),
+            "layout": {"pad_words": a.pad_words, "field_stride_bytes": 16 * (W + a.pad_words),
+                       "note": "each party's 5 ODO fields are rows of one slab (device-generated)"},
             "world_size": world,
             "backend": dist.get_backend() if distributed else None,
             "verified": ok,
