@@ -26,6 +26,7 @@ def rows(path):
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
     return name.split("(")[0].split("<")[0].split("::")[-1].strip()
 
 

@@ -14,11 +14,18 @@ import json
 import os
 
 
+def kernel_short(name):
+    """'void amph::(anonymous namespace)::k_rv<2, true, true>(...)' or a
+    truncated 'k_rv' -> 'k_rv'."""
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return name.split("(")[0].split("<")[0].split("::")[-1].strip()
+
+
 def per_kernel(path, counter):
     vals = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            vals[r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1]].append(float(r["Counter_Value"]))
+            vals[kernel_short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
