@@ -73,19 +73,43 @@ __device__ __forceinline__ uint32_t dec4_values(uint32_t w, uint32_t& valid) {
   return v - ((cls >> 4) & 0x03030303u);  // no borrow: '/' + ROLL = 66 per byte
 }
 
+// The fused wire kernels' form of dec4_values (they are integer-VALU-bound:
+// DESIGN.md §4a'), 21 instructions per 4 characters instead of ~25:
+// * the value path keeps only the low 6 bits of each byte: c + ROLL6[c >> 4]
+//   (ROLL6 = the roll table mod 64) stays below 256 for an ASCII c, so one
+//   plain 32-bit add has no carry between bytes, and the result's low 6 bits
+//   are the decoded value ('/' takes its -3 first, with no borrow); one AND
+//   clears bits 6-7 for the packing dot products;
+// * validity is cls + 0x7F per byte (class bytes are <= 0x35, so no carry
+//   and bit 7 set iff the class is nonzero), ANDed with ~c and the running
+//   accumulator in one v_bitop3.  Non-ASCII or invalid characters may
+//   corrupt their neighbours' values -- the unit is reported invalid then.
+__device__ __forceinline__ uint32_t dec4_values6(uint32_t w, uint32_t& okacc) {
+  const uint32_t l7 = w & 0x07070707u, h7 = (w >> 4) & 0x07070707u;
+  const uint32_t la = __builtin_amdgcn_perm(0x0E0E0E0Eu, 0x0E0E0E0Au, l7);
+  const uint32_t lb = __builtin_amdgcn_perm(0x35040404u, 0x050C0E0Eu, l7);
+  const uint32_t cl = __builtin_amdgcn_perm(lb, la, ((w >> 1) & 0x04040404u) | 0x03020100u);
+  const uint32_t cls = __builtin_amdgcn_perm(0x08040804u, 0x02310000u, h7) & cl;
+  okacc &= (cls + 0x7F7F7F7Fu) & ~w;
+  const uint32_t roll6 = __builtin_amdgcn_perm(0x39393F3Fu, 0x04130000u, h7);
+  return ((w + roll6) - ((cls >> 4) & 0x03030303u)) & 0x3F3F3F3Fu;
+}
+
 // One full 16-character unit (4 groups, no padding) -> its 12 bytes as 3
 // little-endian dwords; returns the offset of the first invalid character in
 // the unit, or 0xFFFFFFFF.  Each group's 24 bits come from two
 // v_dot4_u32_u8 (64 v0 + v1, 64 v2 + v3) and one shift-or, the 12 bytes from
 // three v_perm_b32 straight out of the four groups; validity is one AND per
 // group, the offset is only searched for when some character is bad.
-__device__ __forceinline__ uint32_t dec_unit16(const uint4 v, uint32_t (&o)[3]) {
+// The unit's 12 bytes; its validity is ANDed into ok (bit 7 of every byte
+// stays set iff every character seen so far is in the alphabet), so a caller
+// that decodes many units tests once and locates a bad character only then.
+__device__ __forceinline__ void dec_unit16_ok(const uint4 v, uint32_t (&o)[3], uint32_t& ok) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint32_t g[4], ok = 0x80808080u, val[4];
+  uint32_t g[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint32_t x = dec4_values(w[q], val[q]);
-    ok &= val[q];
+    const uint32_t x = dec4_values6(w[q], ok);
     g[q] = (__builtin_amdgcn_udot4(x, 0x00000140u, 0u, false) << 12) |
            __builtin_amdgcn_udot4(x, 0x01400000u, 0u, false);
   }
@@ -93,11 +117,20 @@ __device__ __forceinline__ uint32_t dec_unit16(const uint4 v, uint32_t (&o)[3]) 
   o[0] = __builtin_amdgcn_perm(g[1], g[0], 0x06000102u);
   o[1] = __builtin_amdgcn_perm(g[2], g[1], 0x05060001u);
   o[2] = __builtin_amdgcn_perm(g[3], g[2], 0x04050600u);
+}
+
+__device__ __forceinline__ uint32_t dec_unit16(const uint4 v, uint32_t (&o)[3]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t ok = 0x80808080u;
+  dec_unit16_ok(v, o, ok);
   if (ok == 0x80808080u) return 0xFFFFFFFFu;
+  // a bad character somewhere (rare): find the first, group by group
   uint32_t firstbad = 0xFFFFFFFFu;
 #pragma unroll
   for (int q = 3; q >= 0; --q) {
-    const uint32_t inv = ~val[q] & 0x80808080u;
+    uint32_t val;
+    (void)dec4_values(w[q], val);
+    const uint32_t inv = ~val & 0x80808080u;
     if (inv) firstbad = 4 * q + (__builtin_ctz(inv) >> 3);
   }
   return firstbad;

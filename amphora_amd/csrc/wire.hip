@@ -82,6 +82,16 @@ struct WireGroups {
   static constexpr int bufs = G >= F ? F : 2 * G;
 };
 
+// A fast-path unit with a bad character (rare): locate the first one and
+// report (party j, field k) in ODO order, then the offset -- the same
+// atomicMin the per-character path makes.
+__device__ __forceinline__ void bad_unit(const uint4 v, int j, int k, size_t nchars, size_t unit,
+                                         unsigned long long* bad) {
+  uint32_t o[3];
+  const uint32_t fb = dec_unit16(v, o);
+  atomicMin(bad, (unsigned long long)((size_t)(5 * j + k) * nchars + 16 * unit + fb));
+}
+
 template <int NP, bool BIG, bool FAST, int BS>
 __device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nchars, uint32_t pad,
                                             size_t words, uint4 (&raw)[5][NP > 0 ? NP : 1],
@@ -99,21 +109,25 @@ __device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nch
     for (int j = 0; j < (NP > 0 ? NP : kMaxParties); ++j) {
       if (NP == 0 && j >= np) break;
       uint32_t o[3];
-      uint32_t fb;
       if constexpr (FAST && NP > 0) {
         if constexpr (kWirePrefetch > 0) {
           const int ahead = k * NP + j + kWirePrefetch;
           if (ahead < 5 * NP)
             raw[ahead / NP][ahead % NP] = ld(reinterpret_cast<const uint4*>(tx.t[ahead / NP][ahead % NP]) + unit);
         }
-        fb = dec_unit16(raw[k][j], o);
+        uint32_t ok = 0x80808080u;
+        dec_unit16_ok(raw[k][j], o, ok);
+        if (ok != 0x80808080u) bad_unit(raw[k][j], j, k, nchars, unit, bad);
       } else if constexpr (FAST) {
-        fb = dec_unit16(ld(reinterpret_cast<const uint4*>(tx.t[k][j]) + unit), o);
+        const uint4 v = ld(reinterpret_cast<const uint4*>(tx.t[k][j]) + unit);
+        uint32_t ok = 0x80808080u;
+        dec_unit16_ok(v, o, ok);
+        if (ok != 0x80808080u) bad_unit(v, j, k, nchars, unit, bad);
       } else {
-        fb = dec_unit_slow(tx.t[k][j], unit, nchars, pad, o);
+        const uint32_t fb = dec_unit_slow(tx.t[k][j], unit, nchars, pad, o);
+        if (fb != 0xFFFFFFFFu)  // (party j, field k) in ODO order, then the offset
+          atomicMin(bad, (unsigned long long)((size_t)(5 * j + k) * nchars + 16 * unit + fb));
       }
-      if (fb != 0xFFFFFFFFu)  // (party j, field k) in ODO order, then the offset
-        atomicMin(bad, (unsigned long long)((size_t)(5 * j + k) * nchars + 16 * unit + fb));
       uint32_t* l = lds[slot];
       l[3 * threadIdx.x] = o[0];
       l[3 * threadIdx.x + 1] = o[1];
@@ -202,8 +216,18 @@ __device__ __forceinline__ void mask_tile_out(size_t tile, size_t words, const u
 // MAC verify (getSecret, DefaultAmphoraClient.java:206-217 incl. the Jackson
 // base64 decode of every field).  bad: min (5 party + field) * nchars + offset
 // of an invalid character.
+// Waves per SIMD the register allocation must allow (0: the compiler's choice).
+#ifndef AMPH_WIRE_WPE
+#define AMPH_WIRE_WPE 0
+#endif
+#if AMPH_WIRE_WPE > 0
+#define AMPH_WIRE_OCC __attribute__((amdgpu_waves_per_eu(AMPH_WIRE_WPE)))
+#else
+#define AMPH_WIRE_OCC
+#endif
+
 template <int NP, bool BIG, int BS>
-__global__ __launch_bounds__(BS) void k_rv_b64(TextSet tx, int n, size_t words, size_t nchars,
+__global__ __launch_bounds__(BS) AMPH_WIRE_OCC void k_rv_b64(TextSet tx, int n, size_t words, size_t nchars,
                                            uint32_t pad, uint4* out_y, unsigned long long* ff,
                                            unsigned long long* bad, Fp f) {
   __shared__ uint32_t lds[WireGroups<NP>::bufs < 2 ? 2 : WireGroups<NP>::bufs][3 * BS];
@@ -234,7 +258,7 @@ __global__ __launch_bounds__(BS) void k_rv_b64(TextSet tx, int n, size_t words, 
 // base64 records of MaskedInputData (out24, staged through LDS and stored as
 // coalesced 16-byte runs).  createSecret, DefaultAmphoraClient.java:150-170.
 template <int NP, bool BIG, int BS>
-__global__ __launch_bounds__(BS) void k_mask_b64(TextSet tx, int n, size_t words, size_t nchars,
+__global__ __launch_bounds__(BS) AMPH_WIRE_OCC void k_mask_b64(TextSet tx, int n, size_t words, size_t nchars,
                                              uint32_t pad, const uint4* secrets, size_t n_secrets,
                                              uint4* out16, char* out24, unsigned long long* ff,
                                              unsigned long long* bad, Fp f) {

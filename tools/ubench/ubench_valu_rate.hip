@@ -1,6 +1,7 @@
 // VALU issue rate (tool): wave-instructions per SIMD-cycle for a few 32-bit
 // integer instructions the wire decode is made of (v_perm_b32, v_xad /
-// v_add_u32, v_and_or, v_dot4_u32_u8) against v_fma_f32, at 8 waves per SIMD
+// v_add_u32, v_and_or, v_dot4_u32_u8) and the field multiply's v_mad_u64_u32
+// and v_mul_lo_u32 against v_fma_f32, at 8 waves per SIMD
 // with 8 independent chains per lane, so nothing but the pipe limits issue.
 // Reports ns per wave-instruction per SIMD and cycles at the measured clock
 // (s_memtime ticks = shader clock, MI355X_MICROARCH.md).
@@ -15,9 +16,10 @@ constexpr int kIters = 4096, kChains = 8;
 template <int OP>
 __global__ __launch_bounds__(256) void k_rate(unsigned* out, unsigned seed, unsigned long long* ticks) {
   unsigned a[kChains];
+  unsigned long long m[kChains];
   float f[kChains];
 #pragma unroll
-  for (int c = 0; c < kChains; ++c) { a[c] = seed ^ (threadIdx.x * 2654435761u + c); f[c] = (float)a[c]; }
+  for (int c = 0; c < kChains; ++c) { a[c] = seed ^ (threadIdx.x * 2654435761u + c); f[c] = (float)a[c]; m[c] = a[c]; }
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int i = 0; i < kIters; ++i) {
 #pragma unroll
@@ -26,13 +28,15 @@ __global__ __launch_bounds__(256) void k_rate(unsigned* out, unsigned seed, unsi
       else if constexpr (OP == 1) a[c] = a[c] + (a[c] ^ seed);   // 2 instructions (v_xor + v_add, or v_xad)
       else if constexpr (OP == 2) a[c] = __builtin_amdgcn_udot4(a[c], 0x01400140u, a[c], false);
       else if constexpr (OP == 3) a[c] = __builtin_amdgcn_alignbit(a[c], a[c] ^ seed, 7);  // v_alignbit_b32 (+ v_xor)
+      else if constexpr (OP == 5) m[c] = (unsigned long long)(unsigned)m[c] * seed + m[c];  // v_mad_u64_u32
+      else if constexpr (OP == 6) a[c] = a[c] * (a[c] | seed);  // v_or + v_mul_lo_u32
       else f[c] = __builtin_fmaf(f[c], 1.0001f, 0.5f);
     }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   unsigned r = 0;
 #pragma unroll
-  for (int c = 0; c < kChains; ++c) r ^= a[c] ^ __float_as_uint(f[c]);
+  for (int c = 0; c < kChains; ++c) r ^= a[c] ^ __float_as_uint(f[c]) ^ (unsigned)m[c] ^ (unsigned)(m[c] >> 32);
   out[blockIdx.x * blockDim.x + threadIdx.x] = r;
   if (threadIdx.x == 0 && blockIdx.x == 0) ticks[0] = t1 - t0;
 }
@@ -72,5 +76,7 @@ int main() {
   run<1>("v_xad_u32", 1, cus);
   run<2>("v_dot4_u32_u8", 1, cus);
   run<3>("v_xor_b32+v_alignbit_b32", 2, cus);
+  run<5>("v_mad_u64_u32", 1, cus);
+  run<6>("v_or_b32+v_mul_lo_u32", 2, cus);
   return 0;
 }
