@@ -74,25 +74,44 @@ __device__ __forceinline__ uint32_t dec4_values(uint32_t w, uint32_t& valid) {
 }
 
 // The fused wire kernels' form of dec4_values (they are integer-VALU-bound:
-// DESIGN.md §4a'), 21 instructions per 4 characters instead of ~25:
-// * the value path keeps only the low 6 bits of each byte: c + ROLL6[c >> 4]
-//   (ROLL6 = the roll table mod 64) stays below 256 for an ASCII c, so one
-//   plain 32-bit add has no carry between bytes, and the result's low 6 bits
-//   are the decoded value ('/' takes its -3 first, with no borrow); one AND
-//   clears bits 6-7 for the packing dot products;
-// * validity is cls + 0x7F per byte (class bytes are <= 0x35, so no carry
-//   and bit 7 set iff the class is nonzero), ANDed with ~c and the running
-//   accumulator in one v_bitop3.  Non-ASCII or invalid characters may
-//   corrupt their neighbours' values -- the unit is reported invalid then.
-__device__ __forceinline__ uint32_t dec4_values6(uint32_t w, uint32_t& okacc) {
+// DESIGN.md §4a'), 19 instructions per 4 characters instead of ~25:
+// * the value path keeps only the low 6 bits of each byte: c + ROLL6[.]
+//   (the roll table mod 64) stays below 256 for an ASCII c, so one plain
+//   32-bit add has no carry between bytes, and its low 6 bits are the value;
+//   one AND clears bits 6-7 for the packing dot products;
+// * '/' needs its own roll (16; '+' 19): the class tables give '/' -- and only
+//   '/' -- bit 1 of its class byte (HI[2] and LO[15] are the only entries
+//   holding it), and the roll lookup's selector is h ^ (class & 2), which
+//   sends '/' to slot 0 (h = 0 is a control character, so slot 0 is free);
+// * validity is class + 0x7F per byte (class bytes are <= 0x1C: no carry,
+//   bit 7 set iff the class is nonzero), ANDed with ~c into the running mask.
+// Classes: bit 0 '+' '/' (h 2), bit 1 '/', bit 2 h 4 / 6, bit 3 h 5 / 7,
+// bit 4 digits (h 3); LO[l] holds the groups whose row allows nibble l.
+// Non-ASCII or invalid characters may corrupt their neighbours' values (a
+// carry out of the byte) -- the unit is reported invalid then.
+// The low dwords of its four v_perm tables: a v_perm takes one SGPR or
+// literal operand, so the second table dword has to be in a VGPR; given as
+// compile-time constants the compiler re-materialises them with a v_mov per
+// unit, dec_tabs_vgpr() makes them opaque values held in four VGPRs instead.
+struct DecTabs {
+  uint32_t la, lb, hi, roll;
+};
+#define AMPH_DEC_TABS {0x1C1C1C18u, 0x050C1C1Cu, 0x10030000u, 0x04130010u}
+__device__ __forceinline__ DecTabs dec_tabs_vgpr() {
+  DecTabs t AMPH_DEC_TABS;
+  asm volatile("" : "+v"(t.la), "+v"(t.lb), "+v"(t.hi), "+v"(t.roll));
+  return t;
+}
+
+__device__ __forceinline__ uint32_t dec4_values6(uint32_t w, uint32_t& okacc, const DecTabs& t) {
   const uint32_t l7 = w & 0x07070707u, h7 = (w >> 4) & 0x07070707u;
-  const uint32_t la = __builtin_amdgcn_perm(0x0E0E0E0Eu, 0x0E0E0E0Au, l7);
-  const uint32_t lb = __builtin_amdgcn_perm(0x35040404u, 0x050C0E0Eu, l7);
+  const uint32_t la = __builtin_amdgcn_perm(0x1C1C1C1Cu, t.la, l7);  // LO[0..7]
+  const uint32_t lb = __builtin_amdgcn_perm(0x07040404u, t.lb, l7);  // LO[8..15]
   const uint32_t cl = __builtin_amdgcn_perm(lb, la, ((w >> 1) & 0x04040404u) | 0x03020100u);
-  const uint32_t cls = __builtin_amdgcn_perm(0x08040804u, 0x02310000u, h7) & cl;
+  const uint32_t cls = __builtin_amdgcn_perm(0x08040804u, t.hi, h7) & cl;
   okacc &= (cls + 0x7F7F7F7Fu) & ~w;
-  const uint32_t roll6 = __builtin_amdgcn_perm(0x39393F3Fu, 0x04130000u, h7);
-  return ((w + roll6) - ((cls >> 4) & 0x03030303u)) & 0x3F3F3F3Fu;
+  const uint32_t roll6 = __builtin_amdgcn_perm(0x39393F3Fu, t.roll, h7 ^ (cls & 0x02020202u));
+  return (w + roll6) & 0x3F3F3F3Fu;
 }
 
 // One full 16-character unit (4 groups, no padding) -> its 12 bytes as 3
@@ -104,12 +123,13 @@ __device__ __forceinline__ uint32_t dec4_values6(uint32_t w, uint32_t& okacc) {
 // The unit's 12 bytes; its validity is ANDed into ok (bit 7 of every byte
 // stays set iff every character seen so far is in the alphabet), so a caller
 // that decodes many units tests once and locates a bad character only then.
-__device__ __forceinline__ void dec_unit16_ok(const uint4 v, uint32_t (&o)[3], uint32_t& ok) {
+__device__ __forceinline__ void dec_unit16_ok(const uint4 v, uint32_t (&o)[3], uint32_t& ok,
+                                              const DecTabs& t = DecTabs AMPH_DEC_TABS) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
   uint32_t g[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint32_t x = dec4_values6(w[q], ok);
+    const uint32_t x = dec4_values6(w[q], ok, t);
     g[q] = (__builtin_amdgcn_udot4(x, 0x00000140u, 0u, false) << 12) |
            __builtin_amdgcn_udot4(x, 0x01400000u, 0u, false);
   }

@@ -103,6 +103,7 @@ __device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nch
   const bool consumer = threadIdx.x < Wire<BS>::words && word < words;
   const int np = NP > 0 ? NP : n;
   int slot = 0;  // LDS buffer of the next field
+  const DecTabs tabs = dec_tabs_vgpr();
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
 #pragma unroll
@@ -116,12 +117,12 @@ __device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nch
             raw[ahead / NP][ahead % NP] = ld(reinterpret_cast<const uint4*>(tx.t[ahead / NP][ahead % NP]) + unit);
         }
         uint32_t ok = 0x80808080u;
-        dec_unit16_ok(raw[k][j], o, ok);
+        dec_unit16_ok(raw[k][j], o, ok, tabs);
         if (ok != 0x80808080u) bad_unit(raw[k][j], j, k, nchars, unit, bad);
       } else if constexpr (FAST) {
         const uint4 v = ld(reinterpret_cast<const uint4*>(tx.t[k][j]) + unit);
         uint32_t ok = 0x80808080u;
-        dec_unit16_ok(v, o, ok);
+        dec_unit16_ok(v, o, ok, tabs);
         if (ok != 0x80808080u) bad_unit(v, j, k, nchars, unit, bad);
       } else {
         const uint32_t fb = dec_unit_slow(tx.t[k][j], unit, nchars, pad, o);
@@ -268,8 +269,6 @@ __global__ __launch_bounds__(BS) AMPH_WIRE_OCC void k_mask_b64(TextSet tx, int n
   uint4 raw[5][NP > 0 ? NP : 1];
   const size_t word = (size_t)blockIdx.x * WW + threadIdx.x;
   const bool has_secret = threadIdx.x < WW && word < n_secrets;
-  uint4 s = make_uint4(0, 0, 0, 0);
-  if (has_secret) s = ld(secrets + word);
   const bool fast = ((size_t)blockIdx.x + 1) * Wire<BS>::chars + 4 <= nchars;
   if (fast) {
     wire_load<NP, BS>(tx, raw, blockIdx.x);
@@ -277,6 +276,10 @@ __global__ __launch_bounds__(BS) AMPH_WIRE_OCC void k_mask_b64(TextSet tx, int n
   } else {
     wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x);
   }
+  // the secret after the decode: loaded up front it held 4 VGPRs through it
+  // (98 -> 5 waves per SIMD lost; the other waves hide this load's latency)
+  uint4 s = make_uint4(0, 0, 0, 0);
+  if (has_secret) s = ld(secrets + word);
   mask_tile_out<NP, BS>(blockIdx.x, words, s, n_secrets, acc, out16, out24, ff, lds, f);
 }
 
