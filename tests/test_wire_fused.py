@@ -238,3 +238,55 @@ def test_wire_kernels_at_baseline_sizes(ctx, n, W):
     assert int(ff.item()) == fault and int(bad.item()) == nf
     del buf, odos, texts
     torch.cuda.empty_cache()
+
+
+_ALPHABET = b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/"
+
+
+def test_b64_every_character_in_every_unit_position(ctx, F):
+    """The fused kernels' decode (b64.hpp dec4_values6: 6-bit value path, '/'
+    routed through the roll selector) character by character, on the fast
+    path (the first workgroup's units): every alphabet character at each of
+    a unit's 16 positions must decode as Python's base64 says -- K_RV's
+    secrets and verdict and K_MASK's masked words equal the oracle on the
+    decoded words -- and each of the 192 other byte values, placed at a
+    different unit position each, must be reported at exactly its offset."""
+    import torch
+    n, W = 2, 1536
+    odos, _ = F.synth_odos(seed=1300, n=n, W=W)
+    base = texts_of(odos)
+    nchars = len(base[0][0])
+    assert 16 * 64 < 16 * 256 <= nchars - 4096  # inside the first (fast) workgroup
+    # unit u, position q holds alphabet[(u + 5 q) % 64]: every character at every position
+    t = bytearray(base[1][0])  # party 1's y field: it reaches K_RV's and K_MASK's outputs
+    for u in range(64):
+        for q in range(16):
+            t[16 * u + q] = _ALPHABET[(u + 5 * q) % 64]
+    texts = [list(o) for o in base]
+    texts[1][0] = bytes(t)
+    words = [list(o) for o in odos]
+    words[1][0] = np.frombuffer(base64.b64decode(bytes(t), validate=True), np.uint8).reshape(W, 16)
+    y, ff, bad = _rv(ctx, texts, W, "device")
+    oy, off = F.recombine_verify([tuple(o) for o in words])
+    # (the replaced words break the MAC: both report the same first word; the
+    # secrets of every word are written either way)
+    assert bad == -1 and ff == off and np.array_equal(y, oy)
+    secrets = F.synth_words(seed=1301, count=W, mont=False)
+    m16, _, ffm, badm = ctx.mask_input_b64(on_device(texts), W, torch.from_numpy(secrets).cuda(), raw=True)
+    torch.cuda.synchronize()
+    exp, offm = F.mask_input(secrets, [tuple(o) for o in words])
+    assert int(badm.item()) == 0x7F7F7F7F7F7F7F7F
+    ffm = int(ffm.item())
+    assert (-1 if ffm == 0x7F7F7F7F7F7F7F7F else ffm) == offm
+    assert np.array_equal(m16.cpu().numpy(), exp)
+    # every other byte value, one call each, at unit (b % 64), position (b % 16)
+    others = [b for b in range(256) if b not in _ALPHABET]
+    assert len(others) == 192
+    for b in others:
+        pos = 16 * (b % 64) + (b % 16)
+        t = bytearray(base[0][4])
+        t[pos] = b
+        texts = [list(o) for o in base]
+        texts[0][4] = bytes(t)
+        _, _, bad = _rv(ctx, texts, W, "device")
+        assert bad == 4 * nchars + pos, (b, pos)
