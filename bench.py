@@ -204,16 +204,31 @@ def scatter_gather_phase(a, A, torch, dist, ctx, rank, world, value_resident):
     from amphora_amd.shard import RootScatterGather
     lib = A._lib
     W, n = a.words, a.parties
-    sg = RootScatterGather(W, 10 * n + 1, 2, device="cuda")
-    full_in = full_out = splain = None
-    if rank == 0:
-        full_in = torch.empty((10 * n + 1, W, 16), dtype=torch.uint8, device="cuda")
-        ctx.synth_odos(seed=21, n=n, words=W, buf=full_in[:5 * n].view(5, n, W, 16))
-        _, _, splain = ctx.synth_odos(seed=22, n=n, words=W, with_plain=True,
-                                      buf=full_in[5 * n:10 * n].view(5, n, W, 16))
-        ctx.synth_words(seed=23, count=W, out=full_in[10 * n])
-        full_out = torch.empty((2, W, 16), dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
+    sg = full_in = full_out = splain = None
+    err = None
+    try:  # every allocation first; the ranks agree before any point-to-point op is posted
+        sg = RootScatterGather(W, 10 * n + 1, 2, device="cuda")
+        if rank == 0:
+            full_in = torch.empty((10 * n + 1, W, 16), dtype=torch.uint8, device="cuda")
+            ctx.synth_odos(seed=21, n=n, words=W, buf=full_in[:5 * n].view(5, n, W, 16))
+            _, _, splain = ctx.synth_odos(seed=22, n=n, words=W, with_plain=True,
+                                          buf=full_in[5 * n:10 * n].view(5, n, W, 16))
+            ctx.synth_words(seed=23, count=W, out=full_in[10 * n])
+            full_out = torch.empty((2, W, 16), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+    except (RuntimeError, MemoryError) as e:  # (torch.OutOfMemoryError is a RuntimeError)
+        err = "%s: %s" % (type(e).__name__, str(e).splitlines()[0][:200] if str(e) else "")
+    failed = torch.tensor([1 if err else 0], dtype=torch.int32,
+                          device="cuda" if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(failed, op=dist.ReduceOp.MAX)
+    if failed.item():
+        # a rank could not set up: skip the phase on every rank (no send or
+        # receive was posted, so nothing is left waiting); the device-resident
+        # line stands
+        del full_in, full_out, splain
+        torch.cuda.empty_cache()
+        return {"skipped": "setup failed on %s: %s" % ("rank 0" if err and rank == 0 else "a rank",
+                                                      err or "see that rank's stderr")}
     count = sg.count
     ff = torch.full((2,), NO_FAIL, dtype=torch.int64, device="cuda")
     ffp = [C.cast(C.c_void_p(ff.data_ptr() + 8 * i), C.POINTER(C.c_int64)) for i in range(2)]
@@ -764,7 +779,7 @@ def main():
     sg = None
     if distributed and a.scaling == "strong" and not a.no_scatter_gather:
         sg = scatter_gather_phase(a, A, torch, dist, ctx, rank, world, resident)
-        if rank == 0:
+        if rank == 0 and "verified" in sg:
             ok = ok and sg["verified"]
     if distributed:
         dist.barrier()

@@ -183,3 +183,44 @@ def test_root_scatter_gather_grouped_two_ranks(tmp_path, W, fault):
     assert ok == "1"
     assert int(g) == fault
     assert int(moved) == (W - (W + 1) // 2) * 23 * 16  # rank 1's shard, 21 arrays out + 2 back
+
+
+def _sg_skip_worker(rank, world, port, result_dir):
+    import json
+    import sys
+    import types
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import amphora_amd as A
+    a = types.SimpleNamespace(words=1 << 10, parties=2, sg_steps=1, sg_warmup=0)
+    # no GPU here: every rank's device allocation fails, and the phase must
+    # return "skipped" on every rank without posting a send or a receive
+    res = bench.scatter_gather_phase(a, A, torch, dist, None, rank, world, 1.0)
+    dist.barrier()  # every rank got here: nothing is left waiting in a point-to-point op
+    with open(os.path.join(result_dir, "r%d" % rank), "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+def test_scatter_gather_phase_skips_together_when_setup_fails(tmp_path):
+    """bench.py's root-held scatter/gather phase allocates everything first and
+    the ranks agree (an all-reduce of a failure flag) before any grouped
+    send/recv is posted: when a rank cannot set up, every rank skips the phase
+    and the device-resident line still prints, instead of one rank waiting
+    forever in a receive the root never posts."""
+    import json
+    import torch
+    import torch.multiprocessing as mp
+    if torch.cuda.is_available():
+        pytest.skip("needs a host without a GPU (the allocation failure is the trigger)")
+    mp.start_processes(_sg_skip_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    r0 = json.load(open(tmp_path / "r0"))
+    r1 = json.load(open(tmp_path / "r1"))
+    assert set(r0) == {"skipped"} and r0["skipped"].startswith("setup failed on rank 0: ")
+    assert set(r1) == {"skipped"}
