@@ -213,11 +213,8 @@ __device__ __forceinline__ void mask_tile_out(size_t tile, size_t words, const u
   }
 }
 
-// K_RV from the wire: the N parties' base64 ODO fields -> canonical secrets,
-// MAC verify (getSecret, DefaultAmphoraClient.java:206-217 incl. the Jackson
-// base64 decode of every field).  bad: min (5 party + field) * nchars + offset
-// of an invalid character.
-// Waves per SIMD the register allocation must allow (0: the compiler's choice).
+// Waves per SIMD the register allocation must allow (0: the compiler's choice;
+// tools/ubench A/B knob, spills below ~96 VGPRs).
 #ifndef AMPH_WIRE_WPE
 #define AMPH_WIRE_WPE 0
 #endif
@@ -227,6 +224,10 @@ __device__ __forceinline__ void mask_tile_out(size_t tile, size_t words, const u
 #define AMPH_WIRE_OCC
 #endif
 
+// K_RV from the wire: the N parties' base64 ODO fields -> canonical secrets,
+// MAC verify (getSecret, DefaultAmphoraClient.java:206-217 incl. the Jackson
+// base64 decode of every field).  bad: min (5 party + field) * nchars + offset
+// of an invalid character.
 template <int NP, bool BIG, int BS>
 __global__ __launch_bounds__(BS) AMPH_WIRE_OCC void k_rv_b64(TextSet tx, int n, size_t words, size_t nchars,
                                            uint32_t pad, uint4* out_y, unsigned long long* ff,
@@ -277,7 +278,7 @@ __global__ __launch_bounds__(BS) AMPH_WIRE_OCC void k_mask_b64(TextSet tx, int n
     wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x);
   }
   // the secret after the decode: loaded up front it held 4 VGPRs through it
-  // (98 -> 5 waves per SIMD lost; the other waves hide this load's latency)
+  // (98 VGPRs: 4 waves per SIMD instead of 5); the other waves hide its latency
   uint4 s = make_uint4(0, 0, 0, 0);
   if (has_secret) s = ld(secrets + word);
   mask_tile_out<NP, BS>(blockIdx.x, words, s, n_secrets, acc, out16, out24, ff, lds, f);
