@@ -89,7 +89,8 @@ __device__ __forceinline__ uint32_t dec4_values(uint32_t w, uint32_t& valid) {
 // bit 4 digits (h 3); LO[l] holds the groups whose row allows nibble l.
 // Non-ASCII or invalid characters may corrupt their neighbours' values (a
 // carry out of the byte) -- the unit is reported invalid then.
-// The low dwords of its four v_perm tables: a v_perm takes one SGPR or
+//
+// DecTabs: the low dwords of its four v_perm tables.  A v_perm takes one SGPR or
 // literal operand, so the second table dword has to be in a VGPR; given as
 // compile-time constants the compiler re-materialises them with a v_mov per
 // unit, dec_tabs_vgpr() makes them opaque values held in four VGPRs instead.
@@ -115,14 +116,12 @@ __device__ __forceinline__ uint32_t dec4_values6(uint32_t w, uint32_t& okacc, co
 }
 
 // One full 16-character unit (4 groups, no padding) -> its 12 bytes as 3
-// little-endian dwords; returns the offset of the first invalid character in
-// the unit, or 0xFFFFFFFF.  Each group's 24 bits come from two
-// v_dot4_u32_u8 (64 v0 + v1, 64 v2 + v3) and one shift-or, the 12 bytes from
-// three v_perm_b32 straight out of the four groups; validity is one AND per
-// group, the offset is only searched for when some character is bad.
-// The unit's 12 bytes; its validity is ANDed into ok (bit 7 of every byte
-// stays set iff every character seen so far is in the alphabet), so a caller
-// that decodes many units tests once and locates a bad character only then.
+// little-endian dwords.  Each group's 24 bits come from two v_dot4_u32_u8
+// (64 v0 + v1, 64 v2 + v3) and one shift-or, the 12 bytes from three
+// v_perm_b32 straight out of the four groups.  The unit's validity is ANDed
+// into ok (bit 7 of every byte stays set iff every character seen so far is
+// in the alphabet), so a caller tests once per unit (or per many units) and
+// locates a bad character only then.
 __device__ __forceinline__ void dec_unit16_ok(const uint4 v, uint32_t (&o)[3], uint32_t& ok,
                                               const DecTabs& t = DecTabs AMPH_DEC_TABS) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -139,6 +138,9 @@ __device__ __forceinline__ void dec_unit16_ok(const uint4 v, uint32_t (&o)[3], u
   o[2] = __builtin_amdgcn_perm(g[3], g[2], 0x04050600u);
 }
 
+// dec_unit16_ok for one unit; returns the offset of the first invalid
+// character in it, or 0xFFFFFFFF (located with the exact dec4_values, whose
+// validity mask is per character whatever the neighbours hold).
 __device__ __forceinline__ uint32_t dec_unit16(const uint4 v, uint32_t (&o)[3]) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
   uint32_t ok = 0x80808080u;
