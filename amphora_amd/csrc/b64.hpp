@@ -1,39 +1,11 @@
 // Base64 group coding shared by the wire codec (codec.hip) and the fused
-// wire-format kernels (kernels.hip): Jackson's Base64Variants.MIME_NO_LINEFEEDS
+// wire-format kernels (wire.hip): Jackson's Base64Variants.MIME_NO_LINEFEEDS
 // alphabet, 4 characters <-> 3 bytes, branch-free SWAR / v_perm table lookups.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace amph {
-
-// 4 base64 chars (little-endian bytes, first char lowest) -> the 24-bit group
-// (first char in the top 6 bits).  inv: bit 7 of byte j set iff char j is
-// not in the alphabet.  Table lookups with v_perm_b32 (8-entry byte tables):
-// class = HI[c >> 4] & LO[c & 15], valid iff nonzero, with the bits
-//   1 '+' '/' (high nibble 2, low B / F)   2 digits (high 3, low 0-9)
-//   4 'A'-'O' 'a'-'o' (high 4 / 6, low 1-15)   8 'P'-'Z' 'p'-'z' (high 5 / 7, low 0-A)
-//   0x10 '/' (low F within high 2);
-// value = c + ROLL[c >> 4] bytewise (carry-free), 3 less for '/'.  ~27 VALU
-// ops per 4 chars (dec6's compare/select chain took ~17 per char).
-__device__ __forceinline__ uint32_t dec4(uint32_t w, uint32_t& inv) {
-  const uint32_t lo = w & 0x0F0F0F0Fu, l7 = lo & 0x07070707u, h7 = (w >> 4) & 0x07070707u;
-  const uint32_t la = __builtin_amdgcn_perm(0x0E0E0E0Eu, 0x0E0E0E0Au, l7);  // LO[0..7]
-  const uint32_t lb = __builtin_amdgcn_perm(0x15040404u, 0x050C0E0Eu, l7);  // LO[8..15]
-  const uint32_t cl = __builtin_amdgcn_perm(lb, la, 0x03020100u | ((lo & 0x08080808u) >> 1));
-  const uint32_t cls = __builtin_amdgcn_perm(0x08040804u, 0x02110000u, h7) & cl;
-  inv = ~(((cls & 0x0F0F0F0Fu) + 0x7F7F7F7Fu) & ~w) & 0x80808080u;
-  const uint32_t roll = __builtin_amdgcn_perm(0xB9B9BFBFu, 0x04130000u, h7);
-  uint32_t v = ((w & 0x7F7F7F7Fu) + (roll & 0x7F7F7F7Fu)) ^ ((w ^ roll) & 0x80808080u);
-  const uint32_t fix = (cls >> 4) & 0x01010101u;
-  v -= fix + (fix << 1);
-  return ((v & 0x3Fu) << 18) | ((v & 0x3F00u) << 4) | ((v >> 10) & 0xFC0u) | (v >> 24);
-}
-
-// group -> its 3 bytes in text order in the low 24 bits
-__device__ __forceinline__ uint32_t group_bytes(uint32_t g) {
-  return __builtin_amdgcn_perm(g, g, 0x0C000102u);
-}
 
 // 24-bit group (first char in the top 6 bits) -> its 4 chars, packed
 // little-endian.  SWAR over the four 6-bit values: idx = (v >= 26) + (v >= 52)
@@ -54,13 +26,17 @@ __device__ __forceinline__ uint32_t enc_group(uint32_t b0, uint32_t b1, uint32_t
 }
 
 
-// 4 base64 chars -> their four 6-bit values (one per byte, same order) and
-// a validity mask (bit 7 of byte j set iff char j is in the alphabet): the
-// table lookups of dec4 without its packing or inverted mask.
-// The '/' class bit of dec4's tables is widened to two bits (HI[2] = 0x31,
-// LO[15] = 0x35), so '/' reads 3 in bits 4-5 of its class and the -3 it
-// needs after the ROLL add is (cls >> 4) & 3 -- no multiply by 3 (which the
-// compiler emitted as a quarter-rate v_mul_lo_u32 per group).
+// 4 base64 chars (little-endian bytes, first char lowest) -> their four
+// 6-bit values (one per byte, same order) and a validity mask (bit 7 of byte
+// j set iff char j is in the alphabet, exact per character whatever its
+// neighbours hold: the class is masked to 4 bits before the +0x7F, and the
+// value add is carry-free).  Table lookups with v_perm_b32 (8-entry byte
+// tables): class = HI[c >> 4] & LO[c & 15], valid iff nonzero, with the bits
+//   1 '+' '/' (high nibble 2, low B / F)   2 digits (high 3, low 0-9)
+//   4 'A'-'O' 'a'-'o' (high 4 / 6, low 1-15)   8 'P'-'Z' 'p'-'z' (high 5 / 7, low 0-A)
+// and '/' marked by 3 in bits 4-5 (HI[2] = 0x31, LO[15] = 0x35), so the -3 it
+// needs after the ROLL add is (cls >> 4) & 3.  The exact locator of the fast
+// paths' rare bad units (dec_unit16); the fast paths use dec4_values6.
 __device__ __forceinline__ uint32_t dec4_values(uint32_t w, uint32_t& valid) {
   const uint32_t lo = w & 0x0F0F0F0Fu, l7 = lo & 0x07070707u, h7 = (w >> 4) & 0x07070707u;
   const uint32_t la = __builtin_amdgcn_perm(0x0E0E0E0Eu, 0x0E0E0E0Au, l7);
