@@ -7,17 +7,61 @@
 
 namespace amph {
 
+// Four 6-bit values (one per byte, first char lowest) -> their 4 chars.
+// idx = (v >= 26) + (v >= 52) + (v >= 62) + (v >= 63) picks the offset
+// to ASCII from a v_perm byte table ('A', 'a' - 26, '0' - 52, '+' - 62,
+// '/' - 63).  The offsets are kept mod 128 (0x41 0x47 0x7C 0x6D 0x70): v + off
+// <= 63 + 0x7C stays below 256, so one plain add has no carry between bytes
+// and its low 7 bits are the character (the mod-256 table needed a
+// 5-instruction carry-free add).
+// The four threshold flags (bit 7 of v + 128 - t) are summed with three
+// v_lerp_u8 (per-byte (a + b) / 2, no carry between bytes): the average of
+// the pairwise averages is idx * 32.
+__device__ __forceinline__ uint32_t enc_chars(uint32_t v) {
+  const uint32_t f26 = (v + 0x66666666u) & 0x80808080u, f52 = (v + 0x4C4C4C4Cu) & 0x80808080u;
+  const uint32_t f62 = (v + 0x42424242u) & 0x80808080u, f63 = (v + 0x41414141u) & 0x80808080u;
+  const uint32_t idx = __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(f26, f52, 0u),
+                                             __builtin_amdgcn_lerp(f62, f63, 0u), 0u) >> 5;
+  const uint32_t off = __builtin_amdgcn_perm(0x00000070u, 0x6D7C4741u, idx);
+  return (v + off) & 0x7F7F7F7Fu;
+}
+
 // 24-bit group (first char in the top 6 bits) -> its 4 chars, packed
-// little-endian.  SWAR over the four 6-bit values: idx = (v >= 26) + (v >= 52)
-// + (v >= 62) + (v >= 63) picks the offset to ASCII from a v_perm byte table
-// ('A', 'a' - 26, '0' - 52, '+' - 62, '/' - 63), added carry-free.
+// little-endian.
 __device__ __forceinline__ uint32_t enc4(uint32_t g) {
-  const uint32_t v = ((g >> 18) & 0x3Fu) | ((g >> 4) & 0x3F00u) | ((g << 10) & 0x3F0000u) |
-                     ((g << 24) & 0x3F000000u);
-  const uint32_t idx = (((v + 0x66666666u) >> 7) & 0x01010101u) + (((v + 0x4C4C4C4Cu) >> 7) & 0x01010101u) +
-                       (((v + 0x42424242u) >> 7) & 0x01010101u) + (((v + 0x41414141u) >> 7) & 0x01010101u);
-  const uint32_t off = __builtin_amdgcn_perm(0x000000F0u, 0xEDFC4741u, idx);
-  return ((v & 0x7F7F7F7Fu) + (off & 0x7F7F7F7Fu)) ^ ((v ^ off) & 0x80808080u);
+  return enc_chars(((g >> 18) & 0x3Fu) | ((g >> 4) & 0x3F00u) | ((g << 10) & 0x3F0000u) |
+                   ((g << 24) & 0x3F000000u));
+}
+
+// Bytes [3Q, 3Q + 3) of the little-endian byte stream w[0..N) (zero past its
+// end) -> their 4 chars, for callers that hold the bytes as dwords.  The four
+// 6-bit values come out of two v_perm (the group's bytes b0 b1 b2 arranged as
+// 16-bit lanes b0 | b1:b2 and b0:b1 | b2, zero bytes by selector 0x0C) and two
+// packed 16-bit shifts with a shift count per lane (>> {2, 6}, << {4, 8}):
+// 6 instructions where gathering the bytes into a 24-bit group and
+// spreading it took ~12.
+typedef unsigned short b64_u16x2 __attribute__((ext_vector_type(2)));
+template <int Q, int N>
+__device__ __forceinline__ uint32_t enc_group_w(const uint32_t (&w)[N]) {
+  constexpr int B = 3 * Q, i = B / 4;
+  constexpr uint32_t b0 = B % 4, b1 = b0 + 1, b2 = b0 + 2;  // byte positions in (hi : lo)
+  static_assert(i < N, "group past the stream");
+  uint32_t hi = 0u;
+  if constexpr (i + 1 < N) hi = w[i + 1];
+  const uint32_t lo = w[i];
+  const uint32_t s1 = __builtin_amdgcn_perm(hi, lo, b0 | 0x0C00u | (b2 << 16) | (b1 << 24));  // b0 0 | b2 b1
+  const uint32_t s2 = __builtin_amdgcn_perm(hi, lo, b1 | (b0 << 8) | (b2 << 16) | 0x0C000000u);  // b1 b0 | b2 0
+  const b64_u16x2 a = __builtin_bit_cast(b64_u16x2, s1) >> (b64_u16x2){2, 6};
+  const b64_u16x2 c = __builtin_bit_cast(b64_u16x2, s2) << (b64_u16x2){4, 8};
+  return enc_chars((__builtin_bit_cast(uint32_t, a) & 0x003F003Fu) | (__builtin_bit_cast(uint32_t, c) & 0x3F003F00u));
+}
+
+// A 12-byte unit (3 dwords) -> its 16 chars (4 dwords)
+__device__ __forceinline__ void enc_unit12(const uint32_t (&w)[3], uint32_t (&g)[4]) {
+  g[0] = enc_group_w<0>(w);
+  g[1] = enc_group_w<1>(w);
+  g[2] = enc_group_w<2>(w);
+  g[3] = enc_group_w<3>(w);
 }
 
 // 3 bytes (big-endian group) -> 4 chars packed little-endian in a uint32
@@ -138,13 +182,12 @@ __device__ __forceinline__ uint32_t dec_unit16(const uint4 v, uint32_t (&o)[3]) 
 // "=="), as 6 little-endian dwords.
 __device__ __forceinline__ void enc_word24(const uint4 v, uint32_t (&g)[6]) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint8_t b[18];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) b[q] = (w[q >> 2] >> (8 * (q & 3))) & 0xFF;
-  b[16] = b[17] = 0;
-#pragma unroll
-  for (int q = 0; q < 6; ++q) g[q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
-  g[5] = (g[5] & 0xFFFFu) | ((uint32_t)'=' << 16) | ((uint32_t)'=' << 24);
+  g[0] = enc_group_w<0>(w);
+  g[1] = enc_group_w<1>(w);
+  g[2] = enc_group_w<2>(w);
+  g[3] = enc_group_w<3>(w);
+  g[4] = enc_group_w<4>(w);
+  g[5] = (enc_group_w<5>(w) & 0xFFFFu) | ((uint32_t)'=' << 16) | ((uint32_t)'=' << 24);
 }
 
 }  // namespace amph

@@ -149,16 +149,8 @@ __global__ __launch_bounds__(kMaxBlock) void k_b64_decode(const char* in, size_t
 __global__ __launch_bounds__(kMaxBlock) void k_b64_words(const uint4* in, size_t words, char* out) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
-    const uint4 v = in[i];
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint8_t b[18];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) b[q] = (w[q >> 2] >> (8 * (q & 3))) & 0xFF;
-    b[16] = b[17] = 0;
     uint32_t g[6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) g[q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
-    g[5] = (g[5] & 0xFFFFu) | ((uint32_t)'=' << 16) | ((uint32_t)'=' << 24);
+    enc_word24(in[i], g);
     uint2* o = reinterpret_cast<uint2*>(out + 24 * i);  // 8-byte aligned when out is
     o[0] = make_uint2(g[0], g[1]);
     o[1] = make_uint2(g[2], g[3]);
@@ -214,16 +206,9 @@ __global__ __launch_bounds__(kB64Block) void k_b64_encode_blk(const uint8_t* in,
     lds[4 * q] = v.x; lds[4 * q + 1] = v.y; lds[4 * q + 2] = v.z; lds[4 * q + 3] = v.w;
   }
   __syncthreads();
-  uint8_t b[12];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const uint32_t x = lds[3 * threadIdx.x + q];
-    b[4 * q] = x & 0xFF; b[4 * q + 1] = (x >> 8) & 0xFF;
-    b[4 * q + 2] = (x >> 16) & 0xFF; b[4 * q + 3] = x >> 24;
-  }
+  const uint32_t w[3] = {lds[3 * threadIdx.x], lds[3 * threadIdx.x + 1], lds[3 * threadIdx.x + 2]};
   uint32_t g[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) g[q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
+  enc_unit12(w, g);
   *reinterpret_cast<uint4*>(out + 16 * t) = make_uint4(g[0], g[1], g[2], g[3]);
 }
 
@@ -253,15 +238,10 @@ __global__ __launch_bounds__(kB64Block) void k_b64_decode_blk(const char* in, ui
 __global__ __launch_bounds__(kB64Block) void k_b64_words_blk(const uint4* in, char* out) {
   __shared__ uint32_t lds[6 * kB64Block];
   const size_t i0 = (size_t)blockIdx.x * kB64Block, i = i0 + threadIdx.x;
-  const uint4 v = ldnt4(in + i);
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint8_t b[18];
+  uint32_t g[6];
+  enc_word24(ldnt4(in + i), g);
 #pragma unroll
-  for (int q = 0; q < 16; ++q) b[q] = (w[q >> 2] >> (8 * (q & 3))) & 0xFF;
-  b[16] = b[17] = 0;
-#pragma unroll
-  for (int q = 0; q < 6; ++q) lds[6 * threadIdx.x + q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
-  lds[6 * threadIdx.x + 5] = (lds[6 * threadIdx.x + 5] & 0xFFFFu) | ((uint32_t)'=' << 16) | ((uint32_t)'=' << 24);
+  for (int q = 0; q < 6; ++q) lds[6 * threadIdx.x + q] = g[q];
   __syncthreads();
   uint4* dst = reinterpret_cast<uint4*>(out + 24 * i0);
   for (int q = threadIdx.x; q < 6 * kB64Block / 4; q += kB64Block)
@@ -292,16 +272,9 @@ __global__ __launch_bounds__(kB64Block) void k_b64_encode_multi(B64Streams st, s
       lds[4 * q] = v.x; lds[4 * q + 1] = v.y; lds[4 * q + 2] = v.z; lds[4 * q + 3] = v.w;
     }
     __syncthreads();
-    uint8_t b[12];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const uint32_t x = lds[3 * threadIdx.x + q];
-      b[4 * q] = x & 0xFF; b[4 * q + 1] = (x >> 8) & 0xFF;
-      b[4 * q + 2] = (x >> 16) & 0xFF; b[4 * q + 3] = x >> 24;
-    }
+    const uint32_t w[3] = {lds[3 * threadIdx.x], lds[3 * threadIdx.x + 1], lds[3 * threadIdx.x + 2]};
     uint32_t g[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) g[q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
+    enc_unit12(w, g);
     st16(out + 16 * t, make_uint4(g[0], g[1], g[2], g[3]));
     return;
   }
