@@ -529,9 +529,12 @@ class Context:
         self._check(lib.amph_base64_encode(self._h, _ptr(a), n, _ptr(out), flags, stream))
         return out if _is_dev(a) else out.tobytes()
 
-    def base64_decode(self, text) -> bytes:
+    def base64_decode(self, text, nbytes: int | None = None) -> bytes:
         """base64 ASCII (str / bytes / uint8 array) -> bytes; raises ValueError on
-        an illegal character or a length not divisible by 4."""
+        an illegal character or a length not divisible by 4.  Device text ->
+        (uint8 tensor, bad-index word); with nbytes (the decoded length the
+        caller expects, e.g. 16 per word of an ODO field) the call is fully
+        asynchronous (no read-back of the padding to size the output)."""
         if isinstance(text, str):
             text = text.encode("ascii", errors="replace")
         a = text if _is_dev(text) else np.frombuffer(bytes(text), np.uint8) \
@@ -540,13 +543,17 @@ class Context:
         flags, stream = self._mode(a)
         out = self._empty(a, (3 * n // 4,))
         ob = C.c_size_t(0)
+        async_dev = _is_dev(a) and nbytes is not None
+        if async_dev and not (n % 4 == 0 and 3 * n // 4 - 2 <= nbytes <= 3 * n // 4):
+            raise ValueError("nbytes %d does not fit a %d-character text" % (nbytes, n))
         bad, badp = self._ff(a)
-        st = lib.amph_base64_decode(self._h, _ptr(a), n, _ptr(out), C.byref(ob), badp, flags, stream)
+        st = lib.amph_base64_decode(self._h, _ptr(a), n, _ptr(out), None if async_dev else C.byref(ob), badp,
+                                    flags, stream)
         if st in (AMPH_E_PARAM, AMPH_E_LEN):
             raise ValueError(lib.amph_last_error().decode())
         self._check(st)
         if _is_dev(a):
-            return out[: ob.value], bad
+            return out[: nbytes if async_dev else ob.value], bad
         return out[: ob.value].tobytes()
 
     def base64_encode_words(self, words16):

@@ -1401,10 +1401,14 @@ int amph_base64_decode(amph_ctx* c, const char* in, size_t nchars, uint8_t* out,
   if (flags & AMPH_F_DEVICE) {
     HIP_TRY(use_device(c->device));
     if (!bad_index) return fail(AMPH_E_PARAM, "bad_index is required");
-    // one 2-byte read-back decides the padding (the only synchronous step)
-    HIP_TRY(read_back((hipStream_t)stream, {{last2, in + nchars - 2, 2}}));
-    const size_t ob = 3 * nchars / 4 - b64_padding(last2);
-    if (out_bytes) *out_bytes = ob;
+    // out_bytes given: one 2-byte read-back decides the padding (the only
+    // synchronous step); null: fully asynchronous, the kernel sizes it
+    size_t ob = amph::kB64PadOnDevice;
+    if (out_bytes) {
+      HIP_TRY(read_back((hipStream_t)stream, {{last2, in + nchars - 2, 2}}));
+      ob = 3 * nchars / 4 - b64_padding(last2);
+      *out_bytes = ob;
+    }
     if (int st = reset_ff_dev(bad_index, flags, (hipStream_t)stream)) return st;
     hipError_t e = amph::launch_b64_decode(in, nchars, out, ob, (unsigned long long*)bad_index,
                                            cfg(c, (hipStream_t)stream, (nchars + 15) / 16));

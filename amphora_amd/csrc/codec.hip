@@ -91,11 +91,17 @@ __global__ __launch_bounds__(kMaxBlock) void k_b64_encode(const uint8_t* in, siz
   }
 }
 
-// nchars % 4 == 0; out_bytes = 3 nchars / 4 - padding; bad = first invalid index
+// nchars % 4 == 0; out_bytes = 3 nchars / 4 - padding, or kB64PadOnDevice
+// with text_end: each lane reads the text's last two characters itself (no
+// host read-back to size the output); bad = first invalid index
 __global__ __launch_bounds__(kMaxBlock) void k_b64_decode(const char* in, size_t nchars,
                                                       uint8_t* out, size_t out_bytes,
                                                       unsigned long long* bad, size_t ibase,
                                                       int text_end) {
+  if (out_bytes == kB64PadOnDevice) {
+    const bool p1 = nchars >= 1 && in[nchars - 1] == '=', p2 = p1 && nchars >= 2 && in[nchars - 2] == '=';
+    out_bytes = 3 * nchars / 4 - (size_t)p1 - (size_t)p2;
+  }
   const size_t units = (nchars + 15) / 16;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < units; t += stride) {
@@ -351,7 +357,8 @@ hipError_t launch_b64_decode(const char* in, size_t nchars, uint8_t* out, size_t
   c1.ev_start = nullptr;
   if (nblk) AMPH_LAUNCH(k_b64_decode_blk, dim3((unsigned)nblk), dim3(kB64Block), c0, in, out, bad);
   AMPH_LAUNCH(k_b64_decode, dim3(grid_n(units - done, c)), dim3(c.block), nblk ? c1 : c, in + 16 * done,
-              nchars - 16 * done, out + 12 * done, out_bytes - 12 * done, bad, 16 * done,
+              nchars - 16 * done, out + 12 * done,
+              out_bytes == kB64PadOnDevice ? kB64PadOnDevice : out_bytes - 12 * done, bad, 16 * done,
               (int)text_end);
   return hipGetLastError();
 }

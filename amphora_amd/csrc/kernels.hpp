@@ -127,7 +127,10 @@ hipError_t launch_b64_encode(const uint8_t* in, size_t nbytes, char* out, const 
 // n <= 5 streams of nbytes each, one launch
 hipError_t launch_b64_encode_multi(const uint8_t* const* in, char* const* out, int n, size_t nbytes,
                                    const LaunchCfg& c);
-// text_end: the range ends the text, so '=' may pad its last two chars
+// text_end: the range ends the text, so '=' may pad its last two chars;
+// out_bytes = kB64PadOnDevice (with text_end): the kernel sizes the output
+// from the text's last two characters itself, no host read-back
+constexpr size_t kB64PadOnDevice = ~(size_t)0;
 hipError_t launch_b64_decode(const char* in, size_t nchars, uint8_t* out, size_t out_bytes,
                              unsigned long long* bad, const LaunchCfg& c, bool text_end = true);
 hipError_t launch_b64_words(const uint4* in, size_t words, char* out, const LaunchCfg& c);

@@ -322,8 +322,12 @@ int amph_open_post(amph_ctx* ctx, const uint8_t* const* diff_mags, const uint8_t
  * encode: out gets 4 * ceil(nbytes / 3) chars.
  * decode: nchars % 4 == 0 (else AMPH_E_LEN); *out_bytes = decoded length;
  *   an illegal character returns AMPH_E_PARAM with *bad_index = its position
- *   (device mode: bad_index is a device word, AMPH_NO_FAILURE if clean; the
- *   call reads the last 2 chars back to size the output).
+ *   (device mode: bad_index is a device word, AMPH_NO_FAILURE if clean; with
+ *   out_bytes non-null the call reads the last 2 chars back to size the
+ *   output -- a stream synchronisation; with out_bytes NULL it is fully
+ *   asynchronous: the kernel sizes the output itself, out must hold
+ *   3 * nchars / 4 bytes and the caller knows the decoded length, e.g.
+ *   16 bytes per word of an ODO field).
  * words: one 16-byte word <-> one 24-char record (per-word base64). */
 int amph_base64_encode(amph_ctx* ctx, const uint8_t* in, size_t nbytes, char* out, uint32_t flags,
                        void* stream);

@@ -95,6 +95,40 @@ def test_base64_roundtrip_lengths(ctx, mode):
             if n:
                 dec, bad = ctx.base64_decode(enc)
                 assert dec.cpu().numpy().tobytes() == raw and int(bad.item()) == 0x7F7F7F7F7F7F7F7F, n
+                # fully asynchronous (no padding read-back): the kernel sizes the output
+                dec2, bad2 = ctx.base64_decode(enc, n)
+                assert dec2.cpu().numpy().tobytes() == raw and int(bad2.item()) == 0x7F7F7F7F7F7F7F7F, n
+                with pytest.raises(ValueError, match="does not fit"):
+                    ctx.base64_decode(enc, n + 3)
+
+
+def test_base64_decode_async_reports_bad_characters(ctx):
+    """The no-read-back device decode reports an illegal character (and '='
+    before the padding) at its index like the synchronous form; a clean
+    padded text writes no byte past its decoded length."""
+    import torch
+    for n in (200, 201, 202, 12 * 300):
+        raw = bytes(range(256)) * (n // 256 + 1)
+        raw = raw[:n]
+        good = base64.b64encode(raw)
+        for pos, ch in ((77, ord("*")), (10, ord("=")), (len(good) - 5, 0x80)):
+            t = bytearray(good)
+            t[pos] = ch
+            d = torch.frombuffer(t, dtype=torch.uint8).cuda()
+            _, bad = ctx.base64_decode(d, n)
+            assert int(bad.item()) == pos, (n, pos)
+        d = torch.frombuffer(bytearray(good), dtype=torch.uint8).cuda()
+        out = torch.full((3 * len(good) // 4,), 0xEE, dtype=torch.uint8, device="cuda")
+        import ctypes as C
+        import amphora_amd as A
+        bad = torch.full((1,), 0, dtype=torch.int64, device="cuda")
+        st = A._lib.lib.amph_base64_decode(ctx._h, d.data_ptr(), len(good), out.data_ptr(), None,
+                                           C.cast(C.c_void_p(bad.data_ptr()), C.POINTER(C.c_int64)),
+                                           A._lib.AMPH_F_DEVICE, C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        assert st == 0 and int(bad.item()) == 0x7F7F7F7F7F7F7F7F
+        o = out.cpu().numpy().tobytes()
+        assert o[:n] == raw and set(o[n:]) <= {0xEE}, n
 
 
 def test_base64_host_batches_and_large(ctx):

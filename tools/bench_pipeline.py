@@ -111,14 +111,14 @@ def party_session(mark):
 
 
 def download(mark):
-    fields = [tuple(ctx.base64_decode(t)[0].view(W, 16) for t in o) for o in b64_odos]
+    fields = [tuple(ctx.base64_decode(t, 16 * W)[0].view(W, 16) for t in o) for o in b64_odos]
     mark("base64_decode_x%d" % (5 * n))
     ctx.recombine_verify(fields)
     mark("k_rv")
 
 
 def upload(mark):
-    fields = [tuple(ctx.base64_decode(t)[0].view(W, 16) for t in o) for o in b64_masks]
+    fields = [tuple(ctx.base64_decode(t, 16 * W)[0].view(W, 16) for t in o) for o in b64_masks]
     mark("base64_decode_x%d" % (5 * n))
     masked, _ = ctx.mask_input(fields, secrets)
     mark("k_mask")
