@@ -50,105 +50,121 @@ __device__ __forceinline__ void st4(uint32_t* p, uint32_t v) {
   else *p = v;
 }
 
-__global__ __launch_bounds__(kMaxBlock) void k_b64_encode(const uint8_t* in, size_t nbytes,
-                                                      char* out) {
-  const size_t units = (nbytes + 11) / 12;
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < units; t += stride) {
-    const size_t base = 12 * t;
-    const size_t rem = nbytes - base < 12 ? nbytes - base : 12;
-    uint8_t b[12];
-    if (rem == 12 && (((uintptr_t)(in + base)) & 3) == 0) {
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(in + base);
+// One 12-byte unit t of a byte stream (the final one may be partial and
+// '='-padded; unaligned buffers byte by byte) -> its 16 chars.
+__device__ __forceinline__ void encode_unit(const uint8_t* in, size_t nbytes, char* out, size_t t) {
+  const size_t base = 12 * t;
+  const size_t rem = nbytes - base < 12 ? nbytes - base : 12;
+  uint8_t b[12];
+  if (rem == 12 && (((uintptr_t)(in + base)) & 3) == 0) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(in + base);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const uint32_t x = __builtin_nontemporal_load(w + q);
-        b[4 * q] = x & 0xFF; b[4 * q + 1] = (x >> 8) & 0xFF;
-        b[4 * q + 2] = (x >> 16) & 0xFF; b[4 * q + 3] = x >> 24;
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 12; ++q) b[q] = (size_t)q < rem ? in[base + q] : 0;
+    for (int q = 0; q < 3; ++q) {
+      const uint32_t x = __builtin_nontemporal_load(w + q);
+      b[4 * q] = x & 0xFF; b[4 * q + 1] = (x >> 8) & 0xFF;
+      b[4 * q + 2] = (x >> 16) & 0xFF; b[4 * q + 3] = x >> 24;
     }
-    uint32_t g[4];
+  } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) g[q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
-    char* o = out + 16 * t;
-    if (rem == 12 && (((uintptr_t)o) & 15) == 0) {
-      st16(o, make_uint4(g[0], g[1], g[2], g[3]));
-    } else {
-      // final partial unit: ceil(rem / 3) groups, '=' for the missing bytes
-      const int groups = (int)((rem + 2) / 3);
-      for (int q = 0; q < groups; ++q) {
-        const int have = (int)rem - 3 * q;  // bytes present in this group (1..3)
-        for (int k = 0; k < 4; ++k) {
-          char ch = (char)((g[q] >> (8 * k)) & 0xFF);
-          if (k >= 2 && have < k) ch = '=';
-          o[4 * q + k] = ch;
-        }
+    for (int q = 0; q < 12; ++q) b[q] = (size_t)q < rem ? in[base + q] : 0;
+  }
+  uint32_t g[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) g[q] = enc_group(b[3 * q], b[3 * q + 1], b[3 * q + 2]);
+  char* o = out + 16 * t;
+  if (rem == 12 && (((uintptr_t)o) & 15) == 0) {
+    st16(o, make_uint4(g[0], g[1], g[2], g[3]));
+  } else {
+    // final partial unit: ceil(rem / 3) groups, '=' for the missing bytes
+    const int groups = (int)((rem + 2) / 3);
+    for (int q = 0; q < groups; ++q) {
+      const int have = (int)rem - 3 * q;  // bytes present in this group (1..3)
+      for (int k = 0; k < 4; ++k) {
+        char ch = (char)((g[q] >> (8 * k)) & 0xFF);
+        if (k >= 2 && have < k) ch = '=';
+        o[4 * q + k] = ch;
       }
     }
   }
 }
 
-// nchars % 4 == 0; out_bytes = 3 nchars / 4 - padding, or kB64PadOnDevice
-// with text_end: each lane reads the text's last two characters itself (no
-// host read-back to size the output); bad = first invalid index
+__global__ __launch_bounds__(kMaxBlock) void k_b64_encode(const uint8_t* in, size_t nbytes,
+                                                      char* out) {
+  const size_t units = (nbytes + 11) / 12;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < units; t += stride)
+    encode_unit(in, nbytes, out, t);
+}
+
+// One 16-character unit t of a text (nchars % 4 == 0; the final unit may be
+// partial and carry '=' padding when text_end) -> its bytes below out_bytes;
+// bad = first invalid index (ibase + offset).
+__device__ __forceinline__ void decode_unit(const char* in, size_t nchars, uint8_t* out, size_t out_bytes,
+                                            unsigned long long* bad, size_t ibase, int text_end, size_t t) {
+  const size_t base = 16 * t;
+  const size_t rem = nchars - base < 16 ? nchars - base : 16;
+  uint8_t c[16];
+  if (rem == 16 && (((uintptr_t)(in + base)) & 15) == 0) {
+    const uint4 v = *reinterpret_cast<const uint4*>(in + base);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) c[q] = (w[q >> 2] >> (8 * (q & 3))) & 0xFF;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) c[q] = (size_t)q < rem ? (uint8_t)in[base + q] : 'A';
+  }
+  uint32_t firstbad = 0xFFFFFFFFu;
+  uint8_t o[12];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const size_t pos = base + 4 * q + k;
+      // '=' is legal only in the last two positions of the whole text
+      const bool pad_ok = text_end && c[4 * q + k] == '=' && pos >= nchars - 2 &&
+                          (pos == nchars - 1 || in[nchars - 1] == '=');
+      v[k] = pad_ok ? 0u : dec6(c[4 * q + k]);
+      if (v[k] == 0xFFu && firstbad == 0xFFFFFFFFu) firstbad = (uint32_t)(4 * q + k);
+    }
+    const uint32_t g = (v[0] << 18) | (v[1] << 12) | (v[2] << 6) | v[3];
+    o[3 * q] = (g >> 16) & 0xFF;
+    o[3 * q + 1] = (g >> 8) & 0xFF;
+    o[3 * q + 2] = g & 0xFF;
+  }
+  if (firstbad != 0xFFFFFFFFu && (size_t)firstbad < rem) atomicMin(bad, (unsigned long long)(ibase + base + firstbad));
+  const size_t ob = 12 * t;
+  uint8_t* op = out + ob;
+  if (ob + 12 <= out_bytes && (((uintptr_t)op) & 3) == 0) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(op);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      st4(w + q, o[4 * q] | (o[4 * q + 1] << 8) | (o[4 * q + 2] << 16) | ((uint32_t)o[4 * q + 3] << 24));
+  } else {
+    for (int q = 0; q < 12; ++q)
+      if (ob + q < out_bytes) op[q] = o[q];
+  }
+}
+
+// out_bytes = kB64PadOnDevice (with text_end): the text's last two characters
+// size the output here (no host read-back)
+__device__ __forceinline__ size_t dev_out_bytes(const char* in, size_t nchars, size_t out_bytes) {
+  if (out_bytes != kB64PadOnDevice) return out_bytes;
+  const bool p1 = nchars >= 1 && in[nchars - 1] == '=', p2 = p1 && nchars >= 2 && in[nchars - 2] == '=';
+  return 3 * nchars / 4 - (size_t)p1 - (size_t)p2;
+}
+
+// nchars % 4 == 0; out_bytes = 3 nchars / 4 - padding (or kB64PadOnDevice
+// with text_end); bad = first invalid index
 __global__ __launch_bounds__(kMaxBlock) void k_b64_decode(const char* in, size_t nchars,
                                                       uint8_t* out, size_t out_bytes,
                                                       unsigned long long* bad, size_t ibase,
                                                       int text_end) {
-  if (out_bytes == kB64PadOnDevice) {
-    const bool p1 = nchars >= 1 && in[nchars - 1] == '=', p2 = p1 && nchars >= 2 && in[nchars - 2] == '=';
-    out_bytes = 3 * nchars / 4 - (size_t)p1 - (size_t)p2;
-  }
+  out_bytes = dev_out_bytes(in, nchars, out_bytes);
   const size_t units = (nchars + 15) / 16;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < units; t += stride) {
-    const size_t base = 16 * t;
-    const size_t rem = nchars - base < 16 ? nchars - base : 16;
-    uint8_t c[16];
-    if (rem == 16 && (((uintptr_t)(in + base)) & 15) == 0) {
-      const uint4 v = *reinterpret_cast<const uint4*>(in + base);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int q = 0; q < 16; ++q) c[q] = (w[q >> 2] >> (8 * (q & 3))) & 0xFF;
-    } else {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) c[q] = (size_t)q < rem ? (uint8_t)in[base + q] : 'A';
-    }
-    uint32_t firstbad = 0xFFFFFFFFu;
-    uint8_t o[12];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const size_t pos = base + 4 * q + k;
-        // '=' is legal only in the last two positions of the whole text
-        const bool pad_ok = text_end && c[4 * q + k] == '=' && pos >= nchars - 2 &&
-                            (pos == nchars - 1 || in[nchars - 1] == '=');
-        v[k] = pad_ok ? 0u : dec6(c[4 * q + k]);
-        if (v[k] == 0xFFu && firstbad == 0xFFFFFFFFu) firstbad = (uint32_t)(4 * q + k);
-      }
-      const uint32_t g = (v[0] << 18) | (v[1] << 12) | (v[2] << 6) | v[3];
-      o[3 * q] = (g >> 16) & 0xFF;
-      o[3 * q + 1] = (g >> 8) & 0xFF;
-      o[3 * q + 2] = g & 0xFF;
-    }
-    if (firstbad != 0xFFFFFFFFu && (size_t)firstbad < rem) atomicMin(bad, (unsigned long long)(ibase + base + firstbad));
-    const size_t ob = 12 * t;
-    uint8_t* op = out + ob;
-    if (ob + 12 <= out_bytes && (((uintptr_t)op) & 3) == 0) {
-      uint32_t* w = reinterpret_cast<uint32_t*>(op);
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        st4(w + q, o[4 * q] | (o[4 * q + 1] << 8) | (o[4 * q + 2] << 16) | ((uint32_t)o[4 * q + 3] << 24));
-    } else {
-      for (int q = 0; q < 12; ++q)
-        if (ob + q < out_bytes) op[q] = o[q];
-    }
-  }
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < units; t += stride)
+    decode_unit(in, nchars, out, out_bytes, bad, ibase, text_end, t);
 }
 
 // 16-byte word -> 24 chars ("...==": 5 full groups + 1 byte)
@@ -203,7 +219,16 @@ __device__ __forceinline__ uint4 ldnt4(const uint4* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-__global__ __launch_bounds__(kB64Block) void k_b64_encode_blk(const uint8_t* in, char* out) {
+// The stream's units past the whole blocks (at most kB64Block, the final one
+// possibly partial) are the LAST workgroup's, one per lane through the
+// per-unit path: one launch per call where a separate tail kernel cost a
+// dispatch (~5 us) per call.
+__global__ __launch_bounds__(kB64Block) void k_b64_encode_blk(const uint8_t* in, char* out, size_t nbytes) {
+  if (blockIdx.x + 1 == gridDim.x) {
+    const size_t units = (nbytes + 11) / 12, t = (size_t)blockIdx.x * kB64Block + threadIdx.x;
+    if (t < units) encode_unit(in, nbytes, out, t);
+    return;
+  }
   __shared__ uint32_t lds[3 * kB64Block];
   const size_t u0 = (size_t)blockIdx.x * kB64Block, t = u0 + threadIdx.x;
   const uint4* src = reinterpret_cast<const uint4*>(in + 12 * u0);
@@ -218,8 +243,15 @@ __global__ __launch_bounds__(kB64Block) void k_b64_encode_blk(const uint8_t* in,
   *reinterpret_cast<uint4*>(out + 16 * t) = make_uint4(g[0], g[1], g[2], g[3]);
 }
 
+// (the last workgroup: the remaining units, as k_b64_encode_blk)
 __global__ __launch_bounds__(kB64Block) void k_b64_decode_blk(const char* in, uint8_t* out,
-                                                             unsigned long long* bad) {
+                                                             unsigned long long* bad, size_t nchars,
+                                                             size_t out_bytes, int text_end) {
+  if (blockIdx.x + 1 == gridDim.x) {
+    const size_t units = (nchars + 15) / 16, t = (size_t)blockIdx.x * kB64Block + threadIdx.x;
+    if (t < units) decode_unit(in, nchars, out, dev_out_bytes(in, nchars, out_bytes), bad, 0, text_end, t);
+    return;
+  }
   __shared__ uint32_t lds[3 * kB64Block];
   const size_t u0 = (size_t)blockIdx.x * kB64Block, t = u0 + threadIdx.x;
   const uint4 v = ldnt4(reinterpret_cast<const uint4*>(in) + t);
@@ -321,13 +353,11 @@ hipError_t launch_b64_encode(const uint8_t* in, size_t nbytes, char* out, const 
   if (nbytes == 0) return hipSuccess;
   const size_t units = (nbytes + 11) / 12;
   const size_t nblk = aligned16(in) && aligned16(out) ? (units - 1) / kB64Block : 0;
-  const size_t done = nblk * kB64Block;
-  LaunchCfg c0 = c, c1 = c;
-  c0.ev_stop = nullptr;
-  c1.ev_start = nullptr;
-  if (nblk) AMPH_LAUNCH(k_b64_encode_blk, dim3((unsigned)nblk), dim3(kB64Block), c0, in, out);
-  AMPH_LAUNCH(k_b64_encode, dim3(grid_n(units - done, c)), dim3(c.block), nblk ? c1 : c, in + 12 * done,
-              nbytes - 12 * done, out + 16 * done);
+  if (nblk) {  // whole blocks + the tail as the last workgroup, one launch
+    AMPH_LAUNCH(k_b64_encode_blk, dim3((unsigned)nblk + 1), dim3(kB64Block), c, in, out, nbytes);
+    return hipGetLastError();
+  }
+  AMPH_LAUNCH(k_b64_encode, dim3(grid_n(units, c)), dim3(c.block), c, in, nbytes, out);
   return hipGetLastError();
 }
 
@@ -351,14 +381,12 @@ hipError_t launch_b64_decode(const char* in, size_t nchars, uint8_t* out, size_t
   if (nchars == 0) return hipSuccess;
   const size_t units = (nchars + 15) / 16;
   const size_t nblk = aligned16(in) && aligned16(out) ? (units - 1) / kB64Block : 0;
-  const size_t done = nblk * kB64Block;
-  LaunchCfg c0 = c, c1 = c;
-  c0.ev_stop = nullptr;
-  c1.ev_start = nullptr;
-  if (nblk) AMPH_LAUNCH(k_b64_decode_blk, dim3((unsigned)nblk), dim3(kB64Block), c0, in, out, bad);
-  AMPH_LAUNCH(k_b64_decode, dim3(grid_n(units - done, c)), dim3(c.block), nblk ? c1 : c, in + 16 * done,
-              nchars - 16 * done, out + 12 * done,
-              out_bytes == kB64PadOnDevice ? kB64PadOnDevice : out_bytes - 12 * done, bad, 16 * done,
+  if (nblk) {  // whole blocks + the tail as the last workgroup, one launch
+    AMPH_LAUNCH(k_b64_decode_blk, dim3((unsigned)nblk + 1), dim3(kB64Block), c, in, out, bad, nchars, out_bytes,
+                (int)text_end);
+    return hipGetLastError();
+  }
+  AMPH_LAUNCH(k_b64_decode, dim3(grid_n(units, c)), dim3(c.block), c, in, nchars, out, out_bytes, bad, (size_t)0,
               (int)text_end);
   return hipGetLastError();
 }
