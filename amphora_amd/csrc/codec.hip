@@ -273,7 +273,20 @@ __global__ __launch_bounds__(kB64Block) void k_b64_decode_blk(const char* in, ui
 // Per-word records through LDS: the block's 256 x 24 output chars move as
 // 384 coalesced 16-B stores (the per-lane kernel stores 8 B at a 24-B lane
 // stride): 3.74 -> 4.86 TB/s at 16 Mi words.
-__global__ __launch_bounds__(kB64Block) void k_b64_words_blk(const uint4* in, char* out) {
+// (words % 256 != 0: the last workgroup codes the remaining words per lane)
+__global__ __launch_bounds__(kB64Block) void k_b64_words_blk(const uint4* in, char* out, size_t words) {
+  if ((size_t)(blockIdx.x + 1) * kB64Block > words) {
+    const size_t i = (size_t)blockIdx.x * kB64Block + threadIdx.x;
+    if (i < words) {
+      uint32_t g[6];
+      enc_word24(in[i], g);
+      uint2* o = reinterpret_cast<uint2*>(out + 24 * i);
+      o[0] = make_uint2(g[0], g[1]);
+      o[1] = make_uint2(g[2], g[3]);
+      o[2] = make_uint2(g[4], g[5]);
+    }
+    return;
+  }
   __shared__ uint32_t lds[6 * kB64Block];
   const size_t i0 = (size_t)blockIdx.x * kB64Block, i = i0 + threadIdx.x;
   uint32_t g[6];
@@ -393,14 +406,12 @@ hipError_t launch_b64_decode(const char* in, size_t nchars, uint8_t* out, size_t
 
 hipError_t launch_b64_words(const uint4* in, size_t words, char* out, const LaunchCfg& c) {
   if (words == 0) return hipSuccess;
-  const size_t nblk = aligned16(in) && aligned16(out) ? words / kB64Block : 0, done = nblk * kB64Block;
-  LaunchCfg c0 = c, c1 = c;
-  c0.ev_stop = nullptr;
-  c1.ev_start = nullptr;
-  if (nblk) AMPH_LAUNCH(k_b64_words_blk, dim3((unsigned)nblk), dim3(kB64Block), words > done ? c0 : c, in, out);
-  if (words > done)
-    AMPH_LAUNCH(k_b64_words, dim3(grid_n(words - done, c)), dim3(c.block), nblk ? c1 : c, in + done,
-                words - done, out + 24 * done);
+  if (aligned16(in) && aligned16(out) && words >= (size_t)kB64Block) {  // one launch, tail included
+    AMPH_LAUNCH(k_b64_words_blk, dim3((unsigned)((words + kB64Block - 1) / kB64Block)), dim3(kB64Block), c, in,
+                out, words);
+    return hipGetLastError();
+  }
+  AMPH_LAUNCH(k_b64_words, dim3(grid_n(words, c)), dim3(c.block), c, in, words, out);
   return hipGetLastError();
 }
 
