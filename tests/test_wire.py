@@ -689,3 +689,34 @@ def test_vss_json_malformed_fields_are_client_errors(ctx):
         client.verify_vss_json(util, bodies(lambda j, k: 16 if (j, k) == (1, 2) else 0))
     with pytest.raises(A.AmphoraClientException):  # one whole party a word short
         client.verify_vss_json(util, bodies(lambda j, k: 16 if j == 1 else 0))
+
+
+@pytest.mark.parametrize("nbytes", [12 * 256, 12 * 256 + 1, 12 * 512, 12 * 512 - 2, 12 * 257, 12 * 256 * 3 + 11])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_base64_block_kernels_tail_workgroup(ctx, nbytes, offset):
+    """The block kernels take the stream's remaining units (1..256, the final
+    one partial / padded) as their last workgroup: sizes at and around the
+    256-unit block boundaries, 16-byte-aligned buffers (block path) and a
+    1-byte offset (per-lane path), encode and decode, with the async decode
+    and a bad character placed in the tail workgroup's units."""
+    import torch
+    raw = np.random.default_rng(nbytes + offset).integers(0, 256, nbytes, dtype=np.uint8).tobytes()
+    exp = base64.b64encode(raw)
+    buf = torch.zeros(nbytes + 16, dtype=torch.uint8, device="cuda")
+    t = buf[offset:offset + nbytes]
+    t.copy_(torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda())
+    enc = ctx.base64_encode(t)
+    assert enc.cpu().numpy().tobytes() == exp
+    tb = torch.zeros(len(exp) + 16, dtype=torch.uint8, device="cuda")
+    te = tb[offset:offset + len(exp)]
+    te.copy_(enc)
+    dec, bad = ctx.base64_decode(te)
+    assert dec.cpu().numpy().tobytes() == raw and int(bad.item()) == 0x7F7F7F7F7F7F7F7F
+    dec2, bad2 = ctx.base64_decode(te, nbytes)
+    assert dec2.cpu().numpy().tobytes() == raw and int(bad2.item()) == 0x7F7F7F7F7F7F7F7F
+    pos = len(exp) - 7  # inside the last units
+    bt = bytearray(exp)
+    bt[pos] = ord("#")
+    te.copy_(torch.frombuffer(bt, dtype=torch.uint8).cuda())
+    _, bad3 = ctx.base64_decode(te, nbytes)
+    assert int(bad3.item()) == pos
