@@ -70,12 +70,19 @@ def gather_words(local, words: int, width: int, root: int = 0, group=None):
     return full[:words]
 
 
-def _p2p(ops):
+def _p2p(ops, timeout=None):
     """Run a list of (op, tensor, peer) as ONE batch_isend_irecv group (RCCL:
     one ncclGroupStart/End, every send and receive in flight at once).  gloo
     moves host memory only, so for a gloo rehearsal with device tensors the
     sends are staged through host copies and the receives land in host
-    buffers copied back afterwards."""
+    buffers copied back afterwards.
+
+    `timeout` (seconds): the host blocks until every operation of the batch
+    has completed or the time is up, and then raises (torch's
+    `Work.wait(timeout)`, which for RCCL also blocks the CPU) -- a peer that
+    never posts its half turns into an exception here instead of a stream
+    that never drains."""
+    import datetime
     import torch.distributed as dist
     if not ops:
         return
@@ -88,8 +95,12 @@ def _p2p(ops):
                 back.append((t, h))
             t = h
         staged.append(dist.P2POp(op, t, peer))
+    td = datetime.timedelta(seconds=timeout) if timeout else None
     for req in dist.batch_isend_irecv(staged):
-        req.wait()
+        if td is None:
+            req.wait()
+        elif not req.wait(timeout=td):
+            raise TimeoutError("point-to-point batch not complete after %.0f s" % timeout)
     for dev, h in back:
         dev.copy_(h)
 
@@ -128,7 +139,7 @@ class RootScatterGather:
         import torch.distributed as dist
         return r if self.group is None else dist.get_global_rank(self.group, r)
 
-    def scatter(self, full_in=None):
+    def scatter(self, full_in=None, timeout=None):
         """Root passes its `[n_in, words, width]` arrays; every rank gets the
         `[n_in, count, width]` view of its own shard."""
         import torch.distributed as dist
@@ -139,11 +150,11 @@ class RootScatterGather:
             for r, (rs, rc) in enumerate(self.spans):
                 if r != self.root and rc:
                     ops += [(dist.isend, full_in[a, rs:rs + rc], self._peer(r)) for a in range(self.n_in)]
-            _p2p(ops)
+            _p2p(ops, timeout)
             return full_in[:, s:s + c]
         if c:
             ops = [(dist.irecv, self.inbuf[a, :c], self._peer(self.root)) for a in range(self.n_in)]
-        _p2p(ops)
+        _p2p(ops, timeout)
         return self.inbuf[:, :c]
 
     def out_view(self, full_out=None):
@@ -154,7 +165,7 @@ class RootScatterGather:
             return full_out[:, s:s + c]
         return self.outbuf[:, :c]
 
-    def gather(self, full_out=None):
+    def gather(self, full_out=None, timeout=None):
         """Peers send their `out_view()`; the root receives every peer's
         shard straight into its slice of `full_out` `[n_out, words, width]`."""
         import torch.distributed as dist
@@ -167,7 +178,7 @@ class RootScatterGather:
         elif self.count:
             ops = [(dist.isend, self.outbuf[a, :self.count], self._peer(self.root))
                    for a in range(self.n_out)]
-        _p2p(ops)
+        _p2p(ops, timeout)
         return full_out if self.rank == self.root else None
 
     def moved_bytes(self) -> int:

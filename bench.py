@@ -170,6 +170,21 @@ def parse():
                          "W + PAD words long (PAD = 0: rows exactly 2^k words apart)")
     ap.add_argument("--sg-steps", type=int, default=3)
     ap.add_argument("--sg-warmup", type=int, default=1)
+    ap.add_argument("--sg-timeout", type=float, default=60.0,
+                    help="seconds any one point-to-point batch or collective of the scatter/gather "
+                         "phase may take before the phase is abandoned (its sub-object then says "
+                         "`skipped`, the communicator is aborted and the line still prints)")
+    ap.add_argument("--pg-timeout", type=float, default=180.0,
+                    help="process-group timeout (seconds) for every other collective")
+    ap.add_argument("--inject-sg-fault", choices=["", "error", "hang"], default="",
+                    help=argparse.SUPPRESS)  # tests: rank 1 raises / never posts its gather sends
+    ap.add_argument("--no-host-phase", action="store_true",
+                    help="device mode: skip the PCIe-inclusive host_memory sub-object")
+    ap.add_argument("--host-words", type=int, default=32 << 20,
+                    help="host_memory phase: words per rank (C5's per-GPU share, 2^28 / 8)")
+    ap.add_argument("--host-parties", type=int, default=3)
+    ap.add_argument("--host-steps", type=int, default=3)
+    ap.add_argument("--host-warmup", type=int, default=1)
     a = ap.parse_args()
     if a.workload == "auto":
         a.workload = "c4"
@@ -199,8 +214,14 @@ def scatter_gather_phase(a, A, torch, dist, ctx, rank, world, value_resident):
     output array.  Each direction is ONE grouped point-to-point batch
     (`RootScatterGather`: RCCL ncclGroupStart / ncclSend x peers x arrays /
     ncclRecv / ncclGroupEnd over xGMI); nothing is allocated per step.
-    Returns the `scatter_gather` sub-object of rank 0's line."""
-    import ctypes as C
+    Returns the `scatter_gather` sub-object of rank 0's line.
+
+    Every point-to-point batch and collective after the set-up is bounded by
+    --sg-timeout: a peer that never posts its half (the first RCCL P2P
+    between distinct GPUs is the one path no one-GPU rehearsal executes)
+    becomes `{"skipped": ..., "aborted": true}` on the ranks that saw it,
+    and main() then aborts the communicator instead of tearing it down, so
+    the device-resident and host-memory numbers still print."""
     from amphora_amd.shard import RootScatterGather
     lib = A._lib
     W, n = a.words, a.parties
@@ -230,14 +251,55 @@ def scatter_gather_phase(a, A, torch, dist, ctx, rank, world, value_resident):
         return {"skipped": "setup failed on %s: %s" % ("rank 0" if err and rank == 0 else "a rank",
                                                       err or "see that rank's stderr")}
     count = sg.count
+    T = getattr(a, "sg_timeout", 60.0)
+    inject = getattr(a, "inject_sg_fault", "")
+    try:
+        return _scatter_gather_timed(a, torch, dist, ctx, lib, rank, world, value_resident, sg, full_in,
+                                     full_out, splain, count, T, inject)
+    except Exception as e:  # a P2P batch or collective that timed out or failed (RCCL / gloo error)
+        return {"skipped": "scatter/gather aborted on rank %d: %s: %s" % (
+                    rank, type(e).__name__, (str(e).splitlines() or [""])[0][:300]),
+                "aborted": True, "timeout_s": T}
+
+
+def maybe_inject(inject, rank, world):
+    """Test hook (--inject-sg-fault): rank 1 raises ("error") or silently
+    skips posting its half of the gather ("hang"), as a stuck RCCL peer
+    would.  Returns True when the caller must skip its gather."""
+    if not inject or world < 2 or rank != 1:
+        return False
+    if inject == "error":
+        raise RuntimeError("injected scatter/gather fault on rank 1")
+    return True
+
+
+def guarded_all_reduce(dist, t, op, timeout_s):
+    """all_reduce that gives up after `timeout_s` (raises) instead of blocking
+    for ever when a peer has left the phase."""
+    import datetime
+    w = dist.all_reduce(t, op=op, async_op=True)
+    if not w.wait(timeout=datetime.timedelta(seconds=timeout_s)):
+        raise TimeoutError("all_reduce not complete after %.0f s" % timeout_s)
+    return t
+
+
+def _scatter_gather_timed(a, torch, dist, ctx, lib, rank, world, value_resident, sg, full_in, full_out,
+                          splain, count, T, inject):
+    import ctypes as C
+    n, W = a.parties, a.words
     ff = torch.full((2,), NO_FAIL, dtype=torch.int64, device="cuda")
     ffp = [C.cast(C.c_void_p(ff.data_ptr() + 8 * i), C.POINTER(C.c_int64)) for i in range(2)]
     flags = lib.AMPH_F_DEVICE | lib.AMPH_F_ACCUMULATE
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     structs = {}
+    sync_dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+
+    def barrier():
+        torch.cuda.synchronize()
+        guarded_all_reduce(dist, torch.zeros(1, dtype=torch.int32, device=sync_dev), dist.ReduceOp.MAX, T)
 
     def step():
-        local = sg.scatter(full_in)
+        local = sg.scatter(full_in, timeout=T)
         out = sg.out_view(full_out)
         if count:
             if not structs:  # the shard views never move: build the ODO structs once
@@ -248,22 +310,21 @@ def scatter_gather_phase(a, A, torch, dist, ctx, rank, world, value_resident):
                                            out[0].data_ptr(), ffp[0], flags, stream) == 0
             assert lib.lib.amph_recombine_verify(ctx._h, structs["s"][0], n, out[1].data_ptr(), ffp[1],
                                                  flags, stream) == 0
-        sg.gather(full_out)
+        if not maybe_inject(inject, rank, world):
+            sg.gather(full_out, timeout=T)
 
     for _ in range(a.sg_warmup):
         step()
-    torch.cuda.synchronize()
-    dist.barrier()
+    barrier()
     t0 = time.perf_counter()
     for _ in range(a.sg_steps):
         step()
-    torch.cuda.synchronize()
-    dist.barrier()
+    barrier()
     el = time.perf_counter() - t0
     g = torch.where(ff == NO_FAIL, ff, ff + sg.start)
-    dist.all_reduce(g, op=dist.ReduceOp.MIN)
+    guarded_all_reduce(dist, g, dist.ReduceOp.MIN, T)
     t = torch.tensor([el], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    guarded_all_reduce(dist, t, dist.ReduceOp.MAX, T)
     el = t.item()
     checks = {"honest_verdicts": bool((g == NO_FAIL).all().item())}
     res = None
@@ -290,9 +351,140 @@ def scatter_gather_phase(a, A, torch, dist, ctx, rank, world, value_resident):
                                  "RCCL ncclSend/ncclRecv over xGMI" if dist.get_backend() == "nccl"
                                  else dist.get_backend() + " rehearsal, staged through host memory",
                                  10 * n + 1),
-               "verified": all(checks.values()), "verify_checks": checks}
-    del full_in, full_out, splain
+               "timeout_s": T, "verified": all(checks.values()), "verify_checks": checks}
     return res
+
+
+def host_memory_phase(a, torch, dist, ctx, rank, world, distributed):
+    """PCIe-inclusive rate inside the default line (the
+    reference path starts and ends in host memory, DefaultAmphoraClient.java:
+    150-170,206-217): on every rank, C5's per-GPU share (--host-words,
+    2^28 / 8 = 32 Mi words, --host-parties 3) in page-locked host arrays,
+    streamed through this rank's GPU in --batch-words batches by the two
+    host-pointer calls a client makes (amph_mask_input, then
+    amph_recombine_verify; 3-slot HtoD / kernel / DtoH pipeline), outputs
+    written back to caller-owned page-locked arrays.  One n-party ODO set
+    serves as both the mask and the share ODOs (the bytes moved are the
+    same as with two sets; host RAM per rank stays ~9.5 GiB).
+
+    --host-warmup untimed and --host-steps timed steps, bracketed by a
+    barrier + synchronize, max over ranks; words/s sums every rank's words.
+    A pinned-copy probe of the same link (1 GiB HtoD, 512 MiB DtoH, same
+    arrays) gives the fraction of what the link delivers.  verified: both
+    calls report no MAC failure at every step, every canonical secret equals
+    the generated one, and a 4096-word sample of the masked words equals
+    toGfp((s - y) mod p) recomputed with Python integers
+    (SecretShareUtil.java:65-68).  Returns rank 0's `host_memory`
+    sub-object (None elsewhere)."""
+    import numpy as np
+    from amphora_amd.spdz import TEST_PRIME
+    W, n = a.host_words, a.host_parties
+    sync_dev = "cuda" if distributed and dist.get_backend() == "nccl" else "cpu"
+    arrays, err = [], None
+    try:  # allocate + page-lock first; the ranks agree before anything is timed
+        odos_h = np.empty((5, n, W, 16), np.uint8)
+        sec_h, plain_h, masked_h, ys_h = (np.empty((W, 16), np.uint8) for _ in range(4))
+        for arr in (odos_h, sec_h, plain_h, masked_h, ys_h):
+            ctx.host_register(arr)
+            arrays.append(arr)
+        _, buf, plain = ctx.synth_odos(seed=4000 + rank, n=n, words=W, with_plain=True)
+        torch.from_numpy(odos_h).copy_(buf)
+        torch.from_numpy(plain_h).copy_(plain)
+        del buf, plain
+        torch.from_numpy(sec_h).copy_(ctx.synth_words(seed=5000 + rank, count=W))
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    except Exception as e:  # noqa: BLE001 (page-lock / OOM / HIP error: report, do not lose the line)
+        err = "%s: %s" % (type(e).__name__, (str(e).splitlines() or [""])[0][:200])
+    if distributed:
+        f = torch.tensor([1 if err else 0], dtype=torch.int32, device=sync_dev)
+        dist.all_reduce(f, op=dist.ReduceOp.MAX)
+        if f.item() and not err:
+            err = "set-up failed on another rank"
+    if err:
+        for arr in arrays:
+            ctx.host_unregister(arr)
+        return {"skipped": "rank %d: %s" % (rank, err)} if rank == 0 else None
+    try:
+        ctx.set_batch_words(a.batch_words)
+        odos = [tuple(odos_h[k, j] for k in range(5)) for j in range(n)]
+        # the link itself, same arrays: pinned HtoD / DtoH copies on one stream
+        probe_dev = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+        src = torch.from_numpy(odos_h.reshape(-1)[:1 << 30])
+        dst = torch.from_numpy(masked_h.reshape(-1)[:min(1 << 29, masked_h.nbytes)])
+
+        def copy_rate(fn, nbytes, reps=3):
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            e1.synchronize()
+            return reps * nbytes / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+        htod_link = copy_rate(lambda: probe_dev.copy_(src, non_blocking=True), src.numel())
+        dtoh_link = copy_rate(lambda: dst.copy_(probe_dev[:dst.numel()], non_blocking=True), dst.numel())
+        del probe_dev
+        torch.cuda.empty_cache()
+        ok = True
+        for _ in range(a.host_warmup):
+            ctx.mask_input(odos, sec_h, out=masked_h)
+            ctx.recombine_verify(odos, out=ys_h)
+        masked_h.fill(0)
+        ys_h.fill(0)
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.host_steps):
+            _, f1 = ctx.mask_input(odos, sec_h, out=masked_h)
+            _, f2 = ctx.recombine_verify(odos, out=ys_h)
+            ok &= f1 == -1 and f2 == -1
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        checks = {"honest_verdicts": bool(ok), "secrets_match": bool(np.array_equal(ys_h, plain_h))}
+        idx = np.unique(np.random.default_rng(17).integers(0, W, 4096))
+        R = (1 << 128) % TEST_PRIME
+        good = True
+        for i in idx:
+            s_i = int.from_bytes(sec_h[i].tobytes(), "little")
+            y_i = int.from_bytes(plain_h[i].tobytes(), "little")
+            good &= (((s_i - y_i) % TEST_PRIME) * R % TEST_PRIME).to_bytes(16, "little") == masked_h[i].tobytes()
+        checks["masked_sample_match"] = bool(good)
+        ok = all(checks.values())
+        vals = [el, 0.0 if ok else 1.0, htod_link, dtoh_link]
+        if distributed:
+            t = torch.tensor(vals[:2], dtype=torch.float64, device=sync_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            lk = torch.tensor(vals[2:], dtype=torch.float64, device=sync_dev)
+            dist.all_reduce(lk, op=dist.ReduceOp.MIN)
+            vals = t.tolist() + lk.tolist()
+        el, bad, htod_link, dtoh_link = vals
+        if rank != 0:
+            return None
+        htod_b, dtoh_b = 160 * n + 16, 32  # per word and step: 2 ODO sets + secrets in, 2 outputs out
+        ms = el * 1e3 / a.host_steps
+        htod = htod_b * W * a.host_steps / el / 1e9  # per rank, the slowest rank's time
+        return {"words_per_s": W * world * a.host_steps / el, "ms_per_step": ms,
+                "steps": a.host_steps, "warmup": a.host_warmup,
+                "words_per_rank": W, "parties": n, "batch_words": a.batch_words,
+                "host_bytes_per_step": (htod_b + dtoh_b) * W * world,
+                "host_GBps": (htod_b + dtoh_b) * W * world * a.host_steps / el / 1e9,
+                "htod_GBps_per_rank": round(htod, 2),
+                "link_probe_GBps": {"htod": round(htod_link, 2), "dtoh": round(dtoh_link, 2),
+                                    "note": "pinned copies of 1 GiB / 512 MiB of the same arrays, "
+                                            "min over ranks"},
+                "frac_of_link": round(htod / htod_link, 4),
+                "memory": "page-locked caller arrays (amph_host_register), outputs reused across calls",
+                "workload": "C5 per-GPU share: amph_mask_input + amph_recombine_verify from host "
+                            "memory, %d words x %d parties per rank" % (W, n),
+                "verified": bad == 0.0, "verify_checks": checks}
+    finally:
+        for arr in arrays:
+            ctx.host_unregister(arr)
 
 
 def host_mode(a, A, torch, ctx, dist=None, rank=0, world=1):
@@ -504,7 +696,7 @@ def dry_run(a, world, rank):
     import torch.distributed as dist
     from amphora_amd.shard import shard_range
     if world > 1 or a.dist:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=pg_timeout(a))
     total = a.words if a.scaling == "strong" else a.words * world
     start, count = shard_range(total, rank, world) if a.scaling == "strong" else (rank * a.words, a.words)
     steps = a.warmup + a.steps
@@ -517,42 +709,110 @@ def dry_run(a, world, rank):
         dist.all_reduce(verdicts, op=dist.ReduceOp.MIN)
         dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ranks = [rank_record(torch, rank, local, el.item(), 0.0, 0.0, count)]
     if dist.is_initialized():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         sizes = torch.tensor([count], dtype=torch.int64)
         dist.all_reduce(sizes)
         covered = int(sizes.item())
+        ranks = [None] * world
+        dist.all_gather_object(ranks, rank_record(torch, rank, local, el.item(), 0.0, 0.0, count))
     else:
         covered = count
-    sg_ok = None
+    sg_ok, sg_res = None, None
     if dist.is_initialized() and a.scaling == "strong":
         # the root-held exchange of scatter_gather_phase on a small array:
         # one grouped scatter of 10N+1 arrays, a copy standing in for the
-        # kernels, one grouped gather into the root's preallocated output
+        # kernels, one grouped gather into the root's preallocated output,
+        # bounded by --sg-timeout exactly as on the GPU
         from amphora_amd.shard import RootScatterGather
         n, Ws = a.parties, 4099
         sg = RootScatterGather(Ws, 10 * a.parties + 1, 2)
         full_in = torch.randint(0, 256, (10 * n + 1, Ws, 16), dtype=torch.uint8,
                                 generator=torch.Generator().manual_seed(5)) if rank == 0 else None
         full_out = torch.zeros((2, Ws, 16), dtype=torch.uint8) if rank == 0 else None
-        local = sg.scatter(full_in)
-        out = sg.out_view(full_out)
-        out[0].copy_(local[0])
-        out[1].copy_(local[10 * n])
-        sg.gather(full_out)
-        if rank == 0:
-            sg_ok = bool(torch.equal(full_out[0], full_in[0]) and torch.equal(full_out[1], full_in[10 * n]))
+        try:
+            local = sg.scatter(full_in, timeout=a.sg_timeout)
+            out = sg.out_view(full_out)
+            out[0].copy_(local[0])
+            out[1].copy_(local[10 * n])
+            if not maybe_inject(a.inject_sg_fault, rank, world):
+                sg.gather(full_out, timeout=a.sg_timeout)
+            guarded_all_reduce(dist, torch.zeros(1, dtype=torch.int32), dist.ReduceOp.MAX, a.sg_timeout)
+            if rank == 0:
+                sg_ok = bool(torch.equal(full_out[0], full_in[0]) and torch.equal(full_out[1], full_in[10 * n]))
+        except Exception as e:  # noqa: BLE001 (same guard as scatter_gather_phase)
+            sg_res = {"skipped": "scatter/gather aborted on rank %d: %s: %s" % (
+                          rank, type(e).__name__, (str(e).splitlines() or [""])[0][:300]),
+                      "aborted": True, "timeout_s": a.sg_timeout}
+    aborted = bool(sg_res and sg_res.get("aborted"))
     if rank == 0:
         emit({"metric": METRIC, "value": None, "unit": "words/s", "n_gpus": world, "dry_run": True,
-              "scatter_gather_round_trip": sg_ok,
+              "scatter_gather_round_trip": sg_ok, "scatter_gather": sg_res,
+              "per_rank": ranks, "ranks_summary": ranks_summary(ranks, world),
               "world_size": world, "backend": dist.get_backend() if dist.is_initialized() else None,
               "scaling": a.scaling, "steps": a.steps, "warmup": a.warmup,
               "words_covered": covered, "fault_reported_at": int(verdicts[-1, 1].item()),
               "fault_expected_at": shard_range(total, world - 1, world)[0] + count // 3
               if a.scaling == "strong" else (world - 1) * a.words + count // 3,
               "config": workload_config(a, world)})
-    if dist.is_initialized():
-        dist.destroy_process_group()
+    finish_pg(dist, aborted)
+    return aborted
+
+
+def pg_timeout(a):
+    import datetime
+    return datetime.timedelta(seconds=a.pg_timeout)
+
+
+def finish_pg(dist, aborted):
+    """Normal end: barrier + destroy.  After an abandoned scatter/gather the
+    communicator may hold operations a peer never matched: abort it (RCCL:
+    ncclCommAbort, which also ends the stuck kernels) and skip the barrier
+    and destroy, which would block or raise."""
+    if not dist.is_initialized():
+        return
+    if not aborted:
+        dist.barrier()
+        dist.destroy_process_group()  # every collective is done: the other ranks may exit
+        return
+    try:
+        from torch.distributed.distributed_c10d import _abort_process_group
+        _abort_process_group()
+    except Exception as e:  # noqa: BLE001 (gloo has no abort; the process ends right after)
+        print("bench.py: process-group abort: %s: %s" % (type(e).__name__, e), file=sys.stderr)
+
+
+def exit_after_abort(code):
+    """After an aborted communicator, end the process without running the
+    process group's destructors (they may wait on the abandoned operations).
+    This is a plain exit of this process, nothing is exec'd."""
+    sys.stderr.flush()
+    os._exit(code)
+
+
+def rank_record(torch, rank, local, wall_s, k_mask_ms, k_rv_ms, words):
+    """This rank's identity (PCI address and UUID of the GPU it drove) and
+    its own device-resident timings."""
+    bus = uuid = None
+    if torch.cuda.is_available():  # (--dry-run on a host without a GPU: no identity)
+        p = torch.cuda.get_device_properties(local)
+        bus = "%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        uuid = str(getattr(p, "uuid", ""))
+    return {"rank": rank, "local_rank": local, "pci_bus_id": bus, "uuid": uuid, "words": words,
+            "wall_s": wall_s, "k_mask_ms": round(k_mask_ms, 5), "k_rv_ms": round(k_rv_ms, 5)}
+
+
+def ranks_summary(ranks, pg_world):
+    """min / max over ranks of the kernel times, and whether every rank
+    drove its own GPU."""
+    out = {"pg_world_size": pg_world,
+           "distinct_gpus": len({r["pci_bus_id"] for r in ranks if r["pci_bus_id"] is not None})}
+    for k in ("k_mask_ms", "k_rv_ms", "wall_s"):
+        v = [r[k] for r in ranks]
+        out[k] = {"min": min(v), "max": max(v)}
+    return out
 
 
 def workload_config(a, world):
@@ -578,7 +838,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if a.dry_run:
-        dry_run(a, world, rank)
+        if dry_run(a, world, rank):
+            exit_after_abort(0)
         return
     import torch
     import torch.distributed as dist
@@ -592,10 +853,14 @@ def main():
         print("bench.py: --gpus %d but WORLD_SIZE=%d (measuring %d)" % (a.gpus, world, world),
               file=sys.stderr)
     if distributed:
+        # an explicit timeout on every collective, and RCCL errors / timeouts
+        # cleaned up (communicator aborted) without tearing the process down,
+        # so a stuck phase cannot take the finished numbers with it
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
         if a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout(a))
         else:
-            dist.init_process_group(a.backend)
+            dist.init_process_group(a.backend, timeout=pg_timeout(a))
 
     ctx = A.Context(TEST_PRIME, TEST_R, TEST_RINV, device=local)
     if a.mode == "host":
@@ -696,10 +961,16 @@ def main():
     el = time.perf_counter() - t0
     t_mask = sum(e0.elapsed_ms(e1) for e0, e1 in ev_mask) / ns  # ms per launch
     t_rv = sum(e0.elapsed_ms(e1) for e0, e1 in ev_rv) / ns
+    # which physical GPU this rank drove, and its own timings: every rank's
+    # record reaches rank 0 (the reported times stay the max over ranks)
+    mine = rank_record(torch, rank, local, el, t_mask, t_rv, W)
+    ranks = [mine]
     if distributed:
-        t = torch.tensor([el, t_mask, t_rv], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, t_mask, t_rv = t.tolist()
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        el = max(r["wall_s"] for r in ranks)
+        t_mask = max(r["k_mask_ms"] for r in ranks)
+        t_rv = max(r["k_rv_ms"] for r in ranks)
     ok = bool((verdicts == NO_FAIL).all().item())
     # After the timed region: the same access pattern as K_MASK with no
     # arithmetic (amph_stream_probe), stamped the same way -- what this
@@ -767,6 +1038,9 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "bytes_per_word": bpw, "traffic": traffic},
             "pattern_probe": pattern_probe(probe_ms, n, W, kern),
+            "per_rank": ranks,
+            "ranks_summary": ranks_summary(ranks, dist.get_world_size() if distributed else 1),
+            "host_memory": None,
             "scatter_gather": None,
             "cpu_baseline": None,
         }
@@ -776,16 +1050,34 @@ def main():
     del mask_odos, mbuf, mplain, share_odos, sbuf, splain, secrets, masked, ys, ys2
     del mviews, sviews, mask_arr, share_arr
     torch.cuda.empty_cache()
+    # The PCIe-inclusive rate (C5's per-GPU share from page-locked host
+    # memory), before the scatter/gather phase: nothing it measures depends
+    # on a point-to-point exchange.
+    hm = None
+    if not a.no_host_phase:
+        hm = host_memory_phase(a, torch, dist, ctx, rank, world, distributed)
+        if rank == 0 and "verified" in hm:
+            ok = ok and hm["verified"]
     sg = None
     if distributed and a.scaling == "strong" and not a.no_scatter_gather:
         sg = scatter_gather_phase(a, A, torch, dist, ctx, rank, world, resident)
-        if rank == 0 and "verified" in sg:
+        if rank == 0 and sg and "verified" in sg:
             ok = ok and sg["verified"]
+    aborted = bool(sg and sg.get("aborted"))
     if distributed:
-        dist.barrier()
-        dist.destroy_process_group()  # every collective is done: the other ranks may exit
+        if not aborted:  # a rank that saw the phase abort tells the others (ranks that finished it
+            # wait here at most --sg-timeout, then abort too)
+            flag = torch.zeros(1, dtype=torch.int32, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+            try:
+                guarded_all_reduce(dist, flag, dist.ReduceOp.MAX, a.sg_timeout)
+            except Exception:  # noqa: BLE001
+                aborted = True
+        finish_pg(dist, aborted)
     if rank == 0:
         line["verified"] = ok
+        line["host_memory"] = hm if not a.no_host_phase else {"skipped": "--no-host-phase"}
+        if aborted and sg is not None and "aborted" not in sg:
+            sg = dict(sg, aborted_after=True)
         if sg is not None:
             line["scatter_gather"] = sg
         elif a.scaling == "strong" and not a.no_scatter_gather:
@@ -796,6 +1088,8 @@ def main():
         if not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
         emit(line)
+    if aborted:
+        exit_after_abort(0 if ok else 1)
     if not ok:
         bad = (verdicts != NO_FAIL).any(dim=1).nonzero().flatten().tolist()
         sys.exit("verification failed: checks %r, MAC failures at steps %r" % (checks, bad[:10]))

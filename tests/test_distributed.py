@@ -111,6 +111,44 @@ def test_bench_spawns_ranks_itself(gpus, extra, scaling, words):
     assert line["config"]["workload"].startswith("C4" if scaling == "strong" else "C2")
     assert line["config"]["words_total"] == words
     assert line["scatter_gather_round_trip"] is (True if gpus > 1 and scaling == "strong" else None)
+    # per-rank identity and timings reach rank 0 (SCALE lines are self-identifying)
+    assert [r["rank"] for r in line["per_rank"]] == list(range(gpus))
+    for r in line["per_rank"]:
+        assert {"rank", "local_rank", "pci_bus_id", "uuid", "words", "wall_s", "k_mask_ms", "k_rv_ms"} <= set(r)
+    assert sum(r["words"] for r in line["per_rank"]) == words
+    summ = line["ranks_summary"]
+    assert summ["pg_world_size"] == gpus
+    for k in ("k_mask_ms", "k_rv_ms", "wall_s"):
+        assert summ[k]["min"] <= summ[k]["max"]
+
+
+@pytest.mark.parametrize("fault", ["error", "hang"])
+def test_bench_line_survives_a_failed_scatter_gather(fault):
+    """A point-to-point exchange that fails (rank 1 raises) or never completes
+    (rank 1 never posts its gather sends, as a stuck RCCL peer would) is
+    bounded by --sg-timeout: every rank abandons the phase, the communicator
+    is aborted instead of torn down, and rank 0 still prints its ONE line,
+    with the rest of the line intact and `scatter_gather.skipped` set."""
+    import json
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    argv = [sys.executable, os.path.join(root, "bench.py"), "--dry-run", "--gpus", "2", "--backend", "gloo",
+            "--same-device", "--inject-sg-fault", fault, "--sg-timeout", "5"]
+    t0 = time.time()
+    r = subprocess.run(argv, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert time.time() - t0 < 120
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    sg = line["scatter_gather"]
+    assert sg["aborted"] is True and sg["skipped"].startswith("scatter/gather aborted on rank 0")
+    assert line["scatter_gather_round_trip"] is None
+    assert line["fault_reported_at"] == line["fault_expected_at"]
+    assert len(line["per_rank"]) == 2 and line["words_covered"] == 1 << 26
 
 
 def _sg_worker(rank, world, port, W, fault, result_dir):
