@@ -19,7 +19,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libamphora_hip.so")
 
-AMPH_OK, AMPH_E_VERIFY, AMPH_E_LEN, AMPH_E_PARAM, AMPH_E_HIP, AMPH_E_NOMEM = 0, 1, 2, 3, 4, 5
+AMPH_OK, AMPH_E_VERIFY, AMPH_E_LEN, AMPH_E_PARAM, AMPH_E_HIP, AMPH_E_NOMEM, AMPH_E_RANGE = 0, 1, 2, 3, 4, 5, 6
 AMPH_F_DEVICE = 1
 AMPH_F_ACCUMULATE = 2
 AMPH_NO_FAILURE = 0x7F7F7F7F7F7F7F7F
@@ -40,7 +40,8 @@ def _need(cond: bool, detail: str):
 
 
 _STATUS = {AMPH_E_VERIFY: "verification failed", AMPH_E_LEN: "length invariant",
-           AMPH_E_PARAM: "invalid argument", AMPH_E_HIP: "HIP error", AMPH_E_NOMEM: "out of memory"}
+           AMPH_E_PARAM: "invalid argument", AMPH_E_HIP: "HIP error", AMPH_E_NOMEM: "out of memory",
+           AMPH_E_RANGE: "array index out of range"}
 
 
 def _load():
@@ -72,6 +73,7 @@ def _load():
     L.amph_recombine_verify.argtypes = [vp, vp, i32, vp, i64p, u32, vp]
     L.amph_mask_input.argtypes = [vp, vp, i32, vp, sz, vp, i64p, u32, vp]
     L.amph_recombine.argtypes = [vp, C.POINTER(vp), i32, sz, vp, u32, vp]
+    L.amph_recombine_object.argtypes = [vp, C.POINTER(vp), i32, C.POINTER(sz), vp, u32, vp]
     L.amph_verify.argtypes = [vp, vp, vp, vp, vp, vp, sz, i64p, u32, vp]
     L.amph_verify_message.argtypes = [vp, vp, vp, vp, vp, vp, C.c_char_p, sz]
     L.amph_mask_words.argtypes = [vp, vp, vp, sz, vp, u32, vp]
@@ -127,7 +129,7 @@ lib = _load()
 EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count",
             "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_set_batch_words", "amph_ctx_stats", "amph_strerror",
             "amph_last_error", "amph_version", "amph_recombine_verify", "amph_mask_input",
-            "amph_recombine", "amph_verify", "amph_verify_message", "amph_mask_words", "amph_mask_word_host",
+            "amph_recombine", "amph_recombine_object", "amph_verify", "amph_verify_message", "amph_mask_words", "amph_mask_word_host",
             "amph_to_gfp", "amph_from_gfp", "amph_convert_share", "amph_odo_pre",
             "amph_open_diffs", "amph_odo_post", "amph_open_post", "amph_synth_odos", "amph_synth_words",
             "amph_host_register", "amph_host_unregister", "amph_time_next_launch",
@@ -194,6 +196,16 @@ def words_view(x, width: int = 16):
         a = np.ascontiguousarray(x, dtype=np.uint8)
     n = a.size // width
     return a.reshape(-1)[: n * width].reshape(n, width)
+
+
+def byte_len(x) -> int:
+    """Length in bytes of a word buffer as the caller passed it (a ragged
+    party's array need not hold whole words)."""
+    if _is_dev(x):
+        return x.numel() * x.element_size()
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        return len(x)
+    return int(np.asarray(x).nbytes)
 
 
 def _ptr(x):
@@ -289,13 +301,15 @@ class Context:
         arr = (_AmphOdo * n)()
         views = []
         for j, o in enumerate(odos):
-            fs = [words_view(f) for f in o]
-            if len(fs) != 5 or any(f.shape[0] != fs[0].shape[0] for f in fs):
+            lens = [byte_len(f) for f in o]
+            if len(lens) != 5 or any(b != lens[0] for b in lens):
                 # OutputDeliveryObject's constructor invariant (OutputDeliveryObject.java:90-96)
                 raise AmphoraNativeError(AMPH_E_LEN, "The provided shares must be of the same length")
+            fs = [words_view(f) for f in o]
             views.append(fs)
-            nbytes = fs[0].shape[0] * 16
-            arr[j] = _AmphOdo(*[_ptr(f) for f in fs], nbytes)
+            # the party's own byte length: parties may differ (recombineObject's
+            # ragged semantics, include/amphora.h amph_odo)
+            arr[j] = _AmphOdo(*[_ptr(f) for f in fs], lens[0])
         return arr, views
 
     def _out(self, like, shape, out):
@@ -319,7 +333,7 @@ class Context:
         index on the host path, an int64[1] device tensor on the device path."""
         arr, views = self._odo_structs(odos)
         flags, stream = self._mode(*[f for v in views for f in v])
-        W = views[0][0].shape[0]
+        W = arr[0].nbytes // 16  # party 0's word count (SecretShareUtil.java:75)
         out = self._out(views[0][0], (W, 16), out)
         ff, ffp = self._ff(views[0][0])
         self._check(lib.amph_recombine_verify(self._h, arr, len(odos), _ptr(out), ffp, flags,
@@ -343,6 +357,20 @@ class Context:
         out = self._empty(vs[0], (W, 16))
         ptrs = (C.c_void_p * len(vs))(*[_ptr(v) for v in vs])
         self._check(lib.amph_recombine(self._h, ptrs, len(vs), W * 16, _ptr(out), flags, stream))
+        return out
+
+    def recombine_object(self, shares):
+        """recombineObject exactly (client SecretShareUtil.java:70-90): each
+        party's share array of its own byte length (amph_recombine_object)."""
+        if len(shares) == 0:
+            return np.empty((0, 16), np.uint8)
+        lens = (C.c_size_t * len(shares))(*[byte_len(s) for s in shares])
+        vs = [words_view(s) for s in shares]
+        flags, stream = self._mode(*vs)
+        W = lens[0] // 16
+        out = self._empty(vs[0], (W, 16))
+        ptrs = (C.c_void_p * len(vs))(*[_ptr(v) for v in vs])
+        self._check(lib.amph_recombine_object(self._h, ptrs, len(vs), lens, _ptr(out), flags, stream))
         return out
 
     def verify(self, y, r, u, v, w):
@@ -534,7 +562,11 @@ class Context:
         an illegal character or a length not divisible by 4.  Device text ->
         (uint8 tensor, bad-index word); with nbytes (the decoded length the
         caller expects, e.g. 16 per word of an ODO field) the call is fully
-        asynchronous (no read-back of the padding to size the output)."""
+        asynchronous (no read-back of the padding to size the output).
+        nbytes must then EQUAL the text's decoded length, 3 n / 4 minus its
+        '=' padding: it is only range-checked here (the padding is on the
+        device), and a wrong value returns a slice that cuts decoded bytes
+        (too small) or ends in bytes the kernel never wrote (too large)."""
         if isinstance(text, str):
             text = text.encode("ascii", errors="replace")
         a = text if _is_dev(text) else np.frombuffer(bytes(text), np.uint8) \

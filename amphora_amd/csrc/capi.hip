@@ -706,18 +706,44 @@ int check_ctx(amph_ctx* c) { return c ? AMPH_OK : fail(AMPH_E_PARAM, "null conte
 #define AMPH_NO_HOST_IO(flags) \
   if ((flags) & AMPH_F_HOST_IO) return fail(AMPH_E_PARAM, "AMPH_F_HOST_IO is not accepted by this call")
 
-int odo_words(const amph_odo* odos, int n, size_t* words) {
+// recombineObject's word count and ragged party arrays (client
+// SecretShareUtil.java:75,87-88): W = party 0's length / 16, and party j's
+// word i is Arrays.copyOfRange(share_j, 16 i, 16 i + 16) -- a longer array
+// is cut, a word running past the end of a shorter one is zero-padded, and a
+// word STARTING past the end (16 i > length) throws
+// ArrayIndexOutOfBoundsException (AMPH_E_RANGE).  So only word W-1 can be
+// padded: *ragged says some party ends inside it (16 (W-1) <= length < 16 W).
+// Callers that cannot take a padded word pass ragged = nullptr and get
+// AMPH_E_LEN for it.
+int party_words(const size_t* lens, int n, size_t* words, bool* ragged) {
+  const size_t w = lens[0] / AMPH_WORD_WIDTH;
+  bool rg = false;
+  for (int j = 1; j < n; ++j) {
+    if (lens[j] >= AMPH_WORD_WIDTH * w) continue;
+    if (lens[j] + AMPH_WORD_WIDTH < AMPH_WORD_WIDTH * w)
+      return fail(AMPH_E_RANGE, "Arrays.copyOfRange: word " +
+                                    std::to_string(lens[j] / AMPH_WORD_WIDTH + 1) +
+                                    " starts past the end of party " + std::to_string(j) + "'s " +
+                                    std::to_string(lens[j]) + "-byte share array (" +
+                                    std::to_string(w) + " words from party 0)");
+    rg = true;
+  }
+  if (rg && !ragged) return fail(AMPH_E_LEN, "The provided shares must be of the same length");
+  if (ragged) *ragged = rg;
+  *words = w;
+  return AMPH_OK;
+}
+
+int odo_words(const amph_odo* odos, int n, size_t* words, bool* ragged = nullptr) {
   if (!odos || n < 1 || n > AMPH_MAX_PARTIES)
     return fail(AMPH_E_PARAM, "n_parties must be in [1, 16] with a non-null ODO array");
-  const size_t w = odos[0].nbytes / AMPH_WORD_WIDTH;
-  for (int j = 0; j < n; ++j) {
-    if (odos[j].nbytes / AMPH_WORD_WIDTH < w)
-      return fail(AMPH_E_LEN, "The provided shares must be of the same length");
-    if (w && (!odos[j].secret_shares || !odos[j].r_shares || !odos[j].v_shares ||
-              !odos[j].w_shares || !odos[j].u_shares))
+  size_t lens[AMPH_MAX_PARTIES];
+  for (int j = 0; j < n; ++j) lens[j] = odos[j].nbytes;
+  if (int st = party_words(lens, n, words, ragged)) return st;
+  for (int j = 0; j < n; ++j)
+    if (*words && odos[j].nbytes && (!odos[j].secret_shares || !odos[j].r_shares || !odos[j].v_shares ||
+                   !odos[j].w_shares || !odos[j].u_shares))
       return fail(AMPH_E_PARAM, "null ODO field");
-  }
-  *words = w;
   return AMPH_OK;
 }
 
@@ -761,6 +787,130 @@ int reset_ff_dev(int64_t* ff, uint32_t flags, hipStream_t s) {
   if ((uintptr_t)ff & 7) return fail(AMPH_E_PARAM, "first_fail must be 8-byte aligned");
   if (!(flags & AMPH_F_ACCUMULATE)) HIP_TRY(hipMemsetAsync(ff, 0x7F, sizeof(int64_t), s));
   return AMPH_OK;
+}
+
+// ---- the ragged last word (party_words) --------------------------------------
+// A ragged call runs words [0, W-1) as usual (every party holds them in full)
+// and word W-1 as a one-word call over zero-padded copies of each array's
+// bytes [16 (W-1), length): what Arrays.copyOfRange hands fromGfp.
+
+// Stage array i's bytes [off, min(len[i], off + 16)), zero-padded, into the
+// 16-byte word dst + 16 i.  src: host pointers (flags 0), amph_host_array
+// descriptors (AMPH_F_HOST_IO; read through their callback) or device
+// pointers (AMPH_F_DEVICE: dst is device memory, the copies go on s).
+int stage_tail(const uint8_t* const* src, const size_t* len, int m, size_t off, uint8_t* dst,
+               uint32_t flags, hipStream_t s) {
+  if (flags & AMPH_F_DEVICE) {
+    HIP_TRY(hipMemsetAsync(dst, 0, 16 * (size_t)m, s));
+    for (int i = 0; i < m; ++i) {
+      const size_t nb = std::min<size_t>(16, len[i] - off);
+      if (nb) HIP_TRY(hipMemcpyAsync(dst + 16 * i, src[i] + off, nb, hipMemcpyDeviceToDevice, s));
+    }
+    return AMPH_OK;
+  }
+  std::memset(dst, 0, 16 * (size_t)m);
+  for (int i = 0; i < m; ++i) {
+    const size_t nb = std::min<size_t>(16, len[i] - off);
+    if (!nb) continue;
+    if (flags & AMPH_F_HOST_IO) {
+      const amph_host_array* a = (const amph_host_array*)src[i];
+      if (a->read(a, off, nb, dst + 16 * i)) return fail(AMPH_E_PARAM, "a host-array read callback failed");
+    } else {
+      std::memcpy(dst + 16 * i, src[i] + off, nb);
+    }
+  }
+  return AMPH_OK;
+}
+
+// one host word to / from an output / input argument (descriptor under AMPH_F_HOST_IO)
+int put_word(uint8_t* dst, size_t off, const uint8_t* w, uint32_t flags) {
+  if (flags & AMPH_F_HOST_IO) {
+    const amph_host_array* a = (const amph_host_array*)dst;
+    if (a->write(a, off, 16, w)) return fail(AMPH_E_PARAM, "a host-array write callback failed");
+  } else {
+    std::memcpy(dst + off, w, 16);
+  }
+  return AMPH_OK;
+}
+
+// Device scratch of one ragged call: the staged words and a verdict word.
+struct TailScratch {
+  uint8_t* p = nullptr;
+  hipStream_t s = nullptr;
+  ~TailScratch() {
+    if (p) (void)hipFreeAsync(p, s);
+  }
+};
+
+
+// The ODO calls over ragged parties: `masked` = false runs
+// amph_recombine_verify, true amph_mask_input (n_secrets <= W).
+int ragged_odo_call(amph_ctx* c, const amph_odo* odos, int n, size_t W, bool masked, const uint8_t* secrets,
+                    size_t n_secrets, uint8_t* out, int64_t* first_fail, uint32_t flags, void* stream) {
+  const size_t off = AMPH_WORD_WIDTH * (W - 1);
+  const bool dev = flags & AMPH_F_DEVICE, io = flags & AMPH_F_HOST_IO;
+  hipStream_t s = (hipStream_t)stream;
+  amph_odo head[AMPH_MAX_PARTIES], tail[AMPH_MAX_PARTIES];
+  const uint8_t* src[5 * AMPH_MAX_PARTIES];
+  size_t len[5 * AMPH_MAX_PARTIES];
+  for (int j = 0; j < n; ++j) {
+    head[j] = odos[j];
+    head[j].nbytes = off;
+    for (int k = 0; k < 5; ++k) {
+      src[k * n + j] = odo_field(odos[j], k);
+      len[k * n + j] = odos[j].nbytes;
+    }
+  }
+  // words [0, W-1): secrets below W-1 masked there, word W-1's secret (if
+  // any) in the tail; the rest verify only, as amph_mask_input does
+  const size_t hs = std::min(n_secrets, W - 1), ts = n_secrets == W ? 1 : 0;
+  int64_t hf = -1;
+  int64_t* hff = dev ? first_fail : &hf;
+  const int st = masked ? amph_mask_input(c, head, n, secrets, hs, out, hff, flags, stream)
+                        : amph_recombine_verify(c, head, n, out, hff, flags, stream);
+  if (st != AMPH_OK && st != AMPH_E_VERIFY) return st;
+  auto point = [&](uint8_t* base) {
+    for (int j = 0; j < n; ++j) {
+      tail[j] = amph_odo{base + 16 * (0 * n + j), base + 16 * (1 * n + j), base + 16 * (2 * n + j),
+                         base + 16 * (3 * n + j), base + 16 * (4 * n + j), 16};
+    }
+  };
+  if (dev) {
+    HIP_TRY(use_device(c->device));
+    TailScratch sc;
+    sc.s = s;
+    HIP_TRY(hipMallocAsync((void**)&sc.p, 16 * 5 * (size_t)n + 16, s));
+    int64_t* tf = (int64_t*)(sc.p + 16 * 5 * n);
+    if (int r = stage_tail(src, len, 5 * n, off, sc.p, flags, s)) return r;
+    HIP_TRY(hipMemsetAsync(tf, 0x7F, sizeof(int64_t), s));
+    point(sc.p);
+    const uint32_t tfl = AMPH_F_DEVICE | AMPH_F_ACCUMULATE;
+    const int t = masked ? amph_mask_input(c, tail, n, ts ? secrets + off : nullptr, ts,
+                                           ts ? out + off : nullptr, tf, tfl, stream)
+                         : amph_recombine_verify(c, tail, n, out + off, tf, tfl, stream);
+    if (t != AMPH_OK) return t;
+    hipError_t e = amph::launch_ff_merge((unsigned long long*)first_fail, (const unsigned long long*)tf, W - 1, s);
+    return e == hipSuccess ? AMPH_OK : hip_fail(e, "k_ff_merge");
+  }
+  uint8_t words[16 * 5 * AMPH_MAX_PARTIES], sec[16], res[16];
+  if (int r = stage_tail(src, len, 5 * n, off, words, flags, nullptr)) return r;
+  point(words);
+  if (ts) {
+    if (io) {
+      const amph_host_array* a = (const amph_host_array*)secrets;
+      if (a->read(a, off, 16, sec)) return fail(AMPH_E_PARAM, "a host-array read callback failed");
+    } else {
+      std::memcpy(sec, secrets + off, 16);
+    }
+  }
+  int64_t tf = -1;
+  const int t = masked ? amph_mask_input(c, tail, n, ts ? sec : nullptr, ts, ts ? res : nullptr, &tf, 0, nullptr)
+                       : amph_recombine_verify(c, tail, n, res, &tf, 0, nullptr);
+  if (t != AMPH_OK && t != AMPH_E_VERIFY) return t;
+  if ((!masked || ts) && put_word(out, off, res, flags)) return AMPH_E_PARAM;
+  const int64_t v = st == AMPH_E_VERIFY ? hf : (t == AMPH_E_VERIFY ? (int64_t)(W - 1) : -1);
+  if (first_fail) *first_fail = v;
+  return v >= 0 ? AMPH_E_VERIFY : AMPH_OK;
 }
 
 }  // namespace
@@ -812,6 +962,7 @@ const char* amph_strerror(int status) {
     case AMPH_E_PARAM: return "invalid argument";
     case AMPH_E_HIP: return "HIP runtime error";
     case AMPH_E_NOMEM: return "out of memory";
+    case AMPH_E_RANGE: return "array index out of range";
     default: return "unknown status";
   }
 }
@@ -941,8 +1092,14 @@ int amph_recombine_verify(amph_ctx* c, const amph_odo* odos, int n, uint8_t* out
   if (check_ctx(c)) return AMPH_E_PARAM;
   AMPH_HOST_IO_ENTRY(flags);
   size_t W;
-  if (int st = odo_words(odos, n, &W)) return st;
+  bool ragged;
+  if (int st = odo_words(odos, n, &W, &ragged)) return st;
   if (W && !out_secrets) return fail(AMPH_E_PARAM, "null output");
+  if (ragged) {
+    if (flags & AMPH_F_DEVICE)
+      if (int st = check_dev_odos(odos, n)) return st;
+    return ragged_odo_call(c, odos, n, W, false, nullptr, 0, out_secrets, first_fail, flags, stream);
+  }
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_odos(odos, n)) return st;
     if (int st = check_dev_words({out_secrets})) return st;
@@ -976,10 +1133,16 @@ int amph_mask_input(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* sec
   if (check_ctx(c)) return AMPH_E_PARAM;
   AMPH_HOST_IO_ENTRY(flags);
   size_t W;
-  if (int st = odo_words(odos, n, &W)) return st;
+  bool ragged;
+  if (int st = odo_words(odos, n, &W, &ragged)) return st;
   if (n_secrets > W)
     return fail(AMPH_E_LEN, "more secret words than verified input masks");
   if (n_secrets && (!secrets || !out_masked)) return fail(AMPH_E_PARAM, "null secrets/output");
+  if (ragged) {
+    if (flags & AMPH_F_DEVICE)
+      if (int st = check_dev_odos(odos, n)) return st;
+    return ragged_odo_call(c, odos, n, W, true, secrets, n_secrets, out_masked, first_fail, flags, stream);
+  }
   if (flags & AMPH_F_DEVICE) {
     if (int st = check_dev_odos(odos, n)) return st;
     if (int st = check_dev_words({secrets, out_masked})) return st;
@@ -1056,6 +1219,41 @@ int amph_recombine(amph_ctx* c, const uint8_t* const* shares, int n, size_t nbyt
                        for (int j = 0; j < n; ++j) set.s[j] = din[j];
                        return amph::launch_recombine(set, n, cnt, dout[0], c->f, lc);
                      });
+}
+
+int amph_recombine_object(amph_ctx* c, const uint8_t* const* shares, int n, const size_t* nbytes,
+                          uint8_t* out, uint32_t flags, void* stream) {
+  if (check_ctx(c)) return AMPH_E_PARAM;
+  AMPH_HOST_IO_ENTRY(flags);
+  if (!shares || !nbytes || n < 1 || n > AMPH_MAX_PARTIES)
+    return fail(AMPH_E_PARAM, "n_parties must be in [1, 16] with non-null share and length arrays");
+  size_t W;
+  bool ragged;
+  if (int st = party_words(nbytes, n, &W, &ragged)) return st;
+  if (!ragged) return amph_recombine(c, shares, n, AMPH_WORD_WIDTH * W, out, flags, stream);
+  const size_t off = AMPH_WORD_WIDTH * (W - 1);
+  if (!out) return fail(AMPH_E_PARAM, "null output");
+  for (int j = 0; j < n; ++j)
+    if (!shares[j] && nbytes[j]) return fail(AMPH_E_PARAM, "null share array");
+  if (int st = amph_recombine(c, shares, n, off, out, flags, stream)) return st;
+  const uint8_t* tail[AMPH_MAX_PARTIES];
+  if (flags & AMPH_F_DEVICE) {
+    for (int j = 0; j < n; ++j)
+      if (int st = check_dev_words({shares[j]})) return st;
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(use_device(c->device));
+    TailScratch sc;
+    sc.s = s;
+    HIP_TRY(hipMallocAsync((void**)&sc.p, 16 * (size_t)n, s));
+    if (int st = stage_tail(shares, nbytes, n, off, sc.p, flags, s)) return st;
+    for (int j = 0; j < n; ++j) tail[j] = sc.p + 16 * j;
+    return amph_recombine(c, tail, n, 16, out + off, flags, stream);
+  }
+  uint8_t words[16 * AMPH_MAX_PARTIES], res[16];
+  if (int st = stage_tail(shares, nbytes, n, off, words, flags, nullptr)) return st;
+  for (int j = 0; j < n; ++j) tail[j] = words + 16 * j;
+  if (int st = amph_recombine(c, tail, n, 16, res, 0, nullptr)) return st;
+  return put_word(out, off, res, flags);
 }
 
 int amph_verify(amph_ctx* c, const uint8_t* y, const uint8_t* r, const uint8_t* u,
@@ -2011,12 +2209,19 @@ struct amph_party {
   uint64_t text_len = 0;
   uint32_t have = 0;  // bit j: party j's diffs are on the device (bit 0 after begin)
   const unsigned long long* bad_dev[AMPH_MAX_PARTIES] = {};  // device mode: partner verdict words
+  // device mode: the session's own copies of the partner verdicts, and per
+  // slot an event after the partner call's work (finish may use another stream)
+  DevBuf verdicts;
+  hipEvent_t partner_ev[AMPH_MAX_PARTIES] = {};
   bool finished = false;
   ~amph_party() {
     mem.release();
     tmp.release();
     io.release();
+    verdicts.release();
     for (DevBuf& b : pbuf) b.release();
+    for (hipEvent_t& e : partner_ev)
+      if (e) (void)hipEventDestroy(e);
   }
 };
 
@@ -2367,9 +2572,17 @@ int amph_party_partner_dev(amph_party* p, int slot, const char* text, size_t len
   HIP_TRY(use_device(c->device));
   std::lock_guard<std::mutex> g(c->mu);
   p->dstream = (hipStream_t)stream;
+  if (dev_ensure(c, p->verdicts, sizeof(unsigned long long) * AMPH_MAX_PARTIES) != hipSuccess)
+    return fail(AMPH_E_NOMEM, "partner verdict words");
+  if (!p->partner_ev[slot]) HIP_TRY(hipEventCreateWithFlags(&p->partner_ev[slot], hipEventDisableTiming));
   if (int st = party_decode(p, slot, text, len, (unsigned long long*)bad_index, p->dstream)) return st;
+  // the session's copy of the verdict: the caller's word may be reused once
+  // the stream has passed this call
+  unsigned long long* mine = (unsigned long long*)p->verdicts.p + slot;
+  HIP_TRY(hipMemcpyAsync(mine, bad_index, sizeof(unsigned long long), hipMemcpyDeviceToDevice, p->dstream));
+  HIP_TRY(hipEventRecord(p->partner_ev[slot], p->dstream));
   p->have |= 1u << slot;
-  p->bad_dev[slot] = (const unsigned long long*)bad_index;
+  p->bad_dev[slot] = mine;
   return AMPH_OK;
 }
 
@@ -2391,6 +2604,9 @@ int amph_party_finish_b64_dev(amph_party* p, int is_player0, const char* fields_
   HIP_TRY(use_device(c->device));
   std::lock_guard<std::mutex> g(c->mu);
   p->dstream = (hipStream_t)stream;
+  // every accepted partner call's decode and verdict copy, whatever its stream
+  for (int j = 1; j < p->n; ++j)
+    if (p->bad_dev[j] && p->partner_ev[j]) HIP_TRY(hipStreamWaitEvent(p->dstream, p->partner_ev[j], 0));
   if (int st = party_open_post(p, is_player0, p->dstream)) return st;
   if (int st = party_b64(p, p->dstream)) return st;
   amph::PoisonB64 pz{};

@@ -823,6 +823,21 @@ hipError_t launch_take_words(unsigned long long* dev, unsigned long long* host, 
   return hipGetLastError();
 }
 
+// Ragged-party tail (capi.hip, ragged_*): the verdict of a one-word call over
+// word `base` min-combined into the whole call's first-fail word.
+__global__ void k_ff_merge(unsigned long long* ff, const unsigned long long* tail, unsigned long long base) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t = *tail;
+    if (t != kNoFail) atomicMin(ff, base + t);
+  }
+}
+
+hipError_t launch_ff_merge(unsigned long long* ff, const unsigned long long* tail, size_t base,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_ff_merge, dim3(1), dim3(64), 0, s, ff, tail, (unsigned long long)base);
+  return hipGetLastError();
+}
+
 hipError_t launch_synth_words(uint4* out, size_t count, uint64_t seed, const Fp& f,
                               const LaunchCfg& c) {
   if (count == 0) return hipSuccess;

@@ -83,6 +83,10 @@ hipError_t launch_recombine(const ShareSet& sh, int n, size_t words, uint4* out,
                             const LaunchCfg& c);
 
 // verifySecrets on canonical (LE16) integers: y r == w and v r == u (mod p).
+// min-combine a one-word call's verdict (index 0 or kNoFail) as word `base`
+hipError_t launch_ff_merge(unsigned long long* ff, const unsigned long long* tail, size_t base,
+                           hipStream_t s);
+
 hipError_t launch_verify(const uint4* y, const uint4* r, const uint4* u, const uint4* v,
                          const uint4* w, size_t words, unsigned long long* first_fail,
                          const Fp& f, const LaunchCfg& c);

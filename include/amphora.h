@@ -80,6 +80,8 @@ extern "C" {
 #define AMPH_E_PARAM 3    /* invalid argument / field parameters */
 #define AMPH_E_HIP 4      /* HIP runtime error (see amph_last_error) */
 #define AMPH_E_NOMEM 5    /* device or host allocation failed */
+#define AMPH_E_RANGE 6    /* ArrayIndexOutOfBoundsException (a ragged party's word
+                             starts past its array's end, see amph_odo) */
 
 /* flags */
 #define AMPH_F_DEVICE 0x1u /* all buffers are device pointers; async on `stream` */
@@ -88,19 +90,29 @@ extern "C" {
  * The caller sets it to AMPH_NO_FAILURE once before a run of calls (saves
  * one memset launch per call; used by bench.py and for repeated passes). */
 #define AMPH_F_ACCUMULATE 0x2u
-/* Host arrays behind callbacks: every buffer argument of the call is a
+/* Host arrays behind callbacks: every word-array argument of the call is a
  * `const amph_host_array*` (cast to the argument's pointer type) instead of
  * host memory, and the library moves the words with the descriptors' read /
  * write callbacks as its batched pipeline consumes and produces them (a JNI
  * layer's Get/SetByteArrayRegion: the Java heap is not pinned across the GPU
  * call -- INTEGRATION.md).  Accepted by the word-array calls that stream
  * through the host pipeline: amph_recombine_verify, amph_mask_input,
- * amph_recombine, amph_verify, amph_mask_words, amph_to_gfp, amph_from_gfp,
- * amph_convert_share, amph_odo_pre, amph_open_diffs, amph_odo_post,
- * amph_open_post; refused (AMPH_E_PARAM) by every other call with flags, and
- * exclusive with AMPH_F_DEVICE.  Offsets and sizes are in bytes from the
- * start of the array the descriptor stands for; a call reads only what its
- * word count implies, so the caller checks array lengths first. */
+ * amph_recombine, amph_recombine_object, amph_verify, amph_mask_words,
+ * amph_to_gfp, amph_from_gfp, amph_convert_share, amph_odo_pre,
+ * amph_open_diffs, amph_odo_post, amph_open_post; refused (AMPH_E_PARAM) by
+ * every other call with flags, and exclusive with AMPH_F_DEVICE.
+ * What stays raw host memory under AMPH_F_HOST_IO (read or written on the
+ * calling thread, never through a callback):
+ *   - the MAC key of amph_convert_share (16 bytes, mac_key_le);
+ *   - the containers of per-party arrays: the amph_odo array (its five field
+ *     pointers ARE descriptors, nbytes stays a length), and the `shares` /
+ *     `mags` / `negs` pointer arrays and amph_recombine_object's `nbytes`
+ *     (their entries are descriptors / lengths);
+ *   - first_fail, and every scalar.
+ * Offsets and sizes are in bytes from the start of the array the descriptor
+ * stands for; a call reads only what its word counts and lengths imply (a
+ * ragged party's last word only up to its nbytes), so the caller checks
+ * array lengths first. */
 #define AMPH_F_HOST_IO 0x4u
 typedef struct amph_host_array {
   /* copy `bytes` bytes at byte offset `off` of the array into dst (inputs)
@@ -119,8 +131,18 @@ typedef struct amph_host_array {
 typedef struct amph_ctx amph_ctx;
 
 /* One party's OutputDeliveryObject (amphora-common OutputDeliveryObject.java:55-106):
- * five byte[] of equal length; words = nbytes / 16 (a trailing partial word
- * is ignored, as `length / WORD_WIDTH` does in SecretShareUtil.java:75). */
+ * five byte[] of equal length nbytes.
+ * Parties may differ in length, with recombineObject's semantics (client
+ * SecretShareUtil.java:75,87-88): words W = odos[0].nbytes / 16 (a trailing
+ * partial word is ignored); party j's word i is Arrays.copyOfRange(field,
+ * 16 i, 16 i + 16), so a longer party is cut to W words, a party ending
+ * inside word W-1 (16 (W-1) <= nbytes < 16 W) has that word zero-padded
+ * (it then nearly always fails its MAC check: AMPH_E_VERIFY at W-1), and a
+ * party ending before 16 (W-1) makes a word start past its end:
+ * AMPH_E_RANGE (ArrayIndexOutOfBoundsException), nothing written.
+ * amph_recombine_verify and amph_mask_input take such ragged parties in
+ * every mode; the wire-text calls and amph_stream_probe need equal lengths
+ * (AMPH_E_LEN). */
 typedef struct amph_odo {
   const uint8_t* secret_shares; /* <y>  */
   const uint8_t* r_shares;      /* <r>  */
@@ -231,6 +253,12 @@ int amph_mask_input(amph_ctx* ctx, const amph_odo* mask_odos, int n_parties,
 /* recombineObject for one byte[] field: out[i] = sum_j fromGfp(share_j[i]) mod p. */
 int amph_recombine(amph_ctx* ctx, const uint8_t* const* shares, int n_parties, size_t nbytes,
                    uint8_t* out, uint32_t flags, void* stream);
+/* recombineObject exactly (client SecretShareUtil.java:70-90), parties of
+ * their own lengths nbytes[j]: words = nbytes[0] / 16 and the ragged-party
+ * rules of amph_odo (zero-padded last word, AMPH_E_RANGE).  Equal lengths
+ * are amph_recombine.  Same flags (AMPH_F_DEVICE / AMPH_F_HOST_IO). */
+int amph_recombine_object(amph_ctx* ctx, const uint8_t* const* shares, int n_parties,
+                          const size_t* nbytes, uint8_t* out, uint32_t flags, void* stream);
 
 /* verifySecrets over canonical LE16 integers (argument order of the Java
  * method: secrets, rs, us, vs, ws).  The host must pass w, u < p (a value
@@ -270,7 +298,8 @@ int amph_from_gfp(amph_ctx* ctx, const uint8_t* in, size_t words, uint8_t* out, 
 /* convertToSecretShare: masked (words x 16) + input mask tuples (words x 32,
  * share 0 value || mac) -> SecretShare.data (words x 32, value || mac).
  * mac_key: the party's MAC key as an LE16 integer (reduced mod p by the
- * caller, as new BigInteger(macKey) mod p).  use_zero_input_as_data =
+ * caller, as new BigInteger(macKey) mod p); raw host memory even under
+ * AMPH_F_HOST_IO (never a descriptor).  use_zero_input_as_data =
  * (playerId != 0) in StorageService.createSecret :104-109. */
 int amph_convert_share(amph_ctx* ctx, const uint8_t* masked, const uint8_t* mask_tuples,
                        size_t words, const uint8_t mac_key_le[16], int use_zero_input_as_data,
@@ -474,7 +503,13 @@ void amph_party_free(amph_party* party);
  * finishing.  finish_b64_dev: the five fields as base64 text in the session's
  * device memory, *fields_b64[k] their addresses (amph_party_finish_b64's
  * lengths; valid until amph_party_free) -- the response is sent from there.
- * If any partner's *bad_index reports a failure when finish_b64_dev's
+ * amph_party_partner_dev writes its verdict to *bad_index on `stream` and
+ * the session keeps its own copy (a device word it owns, copied on that
+ * stream, plus an event recorded there): the caller may reuse or free
+ * bad_index once `stream` has passed the call, and finish_b64_dev waits for
+ * every accepted partner call's work (the decoded diffs and the verdict)
+ * even when it runs on another stream.
+ * If any partner's verdict reports a failure when finish_b64_dev's
  * kernels run, the five fields come out poisoned: their first four
  * characters are "!!!!" (no base64 decoder accepts them), so a response sent
  * without checking the verdicts cannot carry values computed from a rejected

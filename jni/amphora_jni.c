@@ -36,6 +36,7 @@
  * Build: jni/Makefile (skipped when no JDK is found -- this image has none).
  */
 #include <jni.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -139,12 +140,34 @@ typedef struct {
   jbyteArray gref;
 } JArr;
 
+/* A native thread must detach before it exits (JNI spec, "Detaching from the
+   VM").  libamphora_hip's staging and device-worker threads are joined when
+   their context is destroyed; a thread-specific key whose destructor detaches
+   runs as each of them exits. */
+static pthread_key_t g_detach_key;
+static pthread_once_t g_detach_once = PTHREAD_ONCE_INIT;
+static int g_detach_ok;
+
+static void detach_at_exit(void* vm) {
+  JavaVM* v = (JavaVM*)vm;
+  (*v)->DetachCurrentThread(v);
+}
+
+static void make_detach_key(void) { g_detach_ok = pthread_key_create(&g_detach_key, detach_at_exit) == 0; }
+
 /* the JNIEnv of whichever thread runs the callback: the calling Java thread,
-   or one of libamphora_hip's staging threads, attached as a daemon on first use */
+   or one of libamphora_hip's staging threads, attached as a daemon on first use
+   (and detached when it exits) */
 static JNIEnv* env_here(JavaVM* vm) {
   JNIEnv* e = NULL;
   if ((*vm)->GetEnv(vm, (void**)&e, JNI_VERSION_1_6) == JNI_OK) return e;
+  pthread_once(&g_detach_once, make_detach_key);
+  if (!g_detach_ok) return NULL; /* could not arrange the detach: do not attach */
   if ((*vm)->AttachCurrentThreadAsDaemon(vm, (void**)&e, NULL) != JNI_OK) return NULL;
+  if (pthread_setspecific(g_detach_key, vm) != 0) {
+    (*vm)->DetachCurrentThread(vm);
+    return NULL;
+  }
   return e;
 }
 

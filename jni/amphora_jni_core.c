@@ -32,18 +32,34 @@ const char* amphj_exception_class(int status) {
     /* OutputDeliveryObject.java:90-96, service SecretShareUtil.java:64-66, Jackson input errors */
     case AMPH_E_LEN:
     case AMPH_E_PARAM: return "java/lang/IllegalArgumentException";
+    /* recombineObject's Arrays.copyOfRange past a shorter party's end (SecretShareUtil.java:87-88) */
+    case AMPH_E_RANGE: return "java/lang/ArrayIndexOutOfBoundsException";
     default: return "java/lang/IllegalStateException"; /* HIP runtime / allocation */
   }
 }
 
 static const char kSameLength[] = "The provided shares must be of the same length";
 
-/* n parties x 5 fields of one length; *words = that length / 16 */
+/* n parties x 5 fields: the five arrays of one party have one length (the
+ * OutputDeliveryObject constructor's invariant, OutputDeliveryObject.java:
+ * 90-96); parties may differ -- recombineObject's semantics (word count from
+ * party 0, ragged partners cut / zero-padded / ArrayIndexOutOfBounds) are
+ * libamphora_hip's (include/amphora.h amph_odo).  *words = party 0's words. */
 static int odo_lengths(int n, const size_t* lens, size_t* words) {
+  if (n < 1 || n > AMPH_MAX_PARTIES) return set_msg(AMPH_E_PARAM, "n_parties must be in [1, 16]");
+  for (int k = 1; k < 5; ++k)
+    for (int j = 0; j < n; ++j)
+      if (lens[k * n + j] != lens[j]) return set_msg(AMPH_E_LEN, kSameLength);
+  *words = lens[0] / AMPH_WORD_WIDTH;
+  return AMPH_OK;
+}
+
+/* base64 field texts: the wire entry points take one word count for every
+ * text (amph_odo_b64), so all 5 n texts must have one length */
+static int text_lengths(int n, const size_t* lens) {
   if (n < 1 || n > AMPH_MAX_PARTIES) return set_msg(AMPH_E_PARAM, "n_parties must be in [1, 16]");
   for (int i = 1; i < 5 * n; ++i)
     if (lens[i] != lens[0]) return set_msg(AMPH_E_LEN, kSameLength);
-  *words = lens[0] / AMPH_WORD_WIDTH;
   return AMPH_OK;
 }
 
@@ -68,14 +84,14 @@ int amphj_ctx_create(const uint8_t* p_le, size_t p_len, const uint8_t* r_le, siz
 
 void amphj_ctx_destroy(void* ctx) { amph_ctx_destroy((amph_ctx*)ctx); }
 
-static void odo_structs(int n, const uint8_t* const* fields, size_t nbytes, amph_odo* odos) {
+static void odo_structs(int n, const uint8_t* const* fields, const size_t* lens, amph_odo* odos) {
   for (int j = 0; j < n; ++j) {
     odos[j].secret_shares = fields[0 * n + j];
     odos[j].r_shares = fields[1 * n + j];
     odos[j].v_shares = fields[2 * n + j];
     odos[j].w_shares = fields[3 * n + j];
     odos[j].u_shares = fields[4 * n + j];
-    odos[j].nbytes = nbytes;
+    odos[j].nbytes = lens[j]; /* party j's own length */
   }
 }
 
@@ -87,7 +103,7 @@ int amphj_recombine_verify(void* ctx, int n, const uint8_t* const* fields, const
   if (lst) return lst;
   if (room(out_len, 16 * W, "the secrets array")) return AMPH_E_LEN;
   amph_odo odos[AMPH_MAX_PARTIES];
-  odo_structs(n, fields, lens[0], odos);
+  odo_structs(n, fields, lens, odos);
   return abi(amph_recombine_verify((amph_ctx*)ctx, odos, n, out, fail, g_io, NULL));
 }
 
@@ -101,7 +117,7 @@ int amphj_mask_input(void* ctx, int n, const uint8_t* const* fields, const size_
   const size_t S = secrets_len / 16;
   if (room(out_len, 16 * S, "the masked-input array")) return AMPH_E_LEN;
   amph_odo odos[AMPH_MAX_PARTIES];
-  odo_structs(n, fields, lens[0], odos);
+  odo_structs(n, fields, lens, odos);
   return abi(amph_mask_input((amph_ctx*)ctx, odos, n, secrets, S, out, fail, g_io, NULL));
 }
 
@@ -109,10 +125,9 @@ int amphj_recombine(void* ctx, int n, const uint8_t* const* shares, const size_t
                     size_t out_len) {
   if (n < 1 || n > AMPH_MAX_PARTIES) return set_msg(AMPH_E_PARAM, "n_parties must be in [1, 16]");
   const size_t W = lens[0] / 16;  /* recombineObject: shares.get(0).length / WORD_WIDTH */
-  for (int j = 1; j < n; ++j)
-    if (lens[j] / 16 < W) return set_msg(AMPH_E_LEN, kSameLength);
   if (room(out_len, 16 * W, "the output array")) return AMPH_E_LEN;
-  return abi(amph_recombine((amph_ctx*)ctx, shares, n, 16 * W, out, g_io, NULL));
+  /* ragged partners: cut / zero-padded / ArrayIndexOutOfBounds, as copyOfRange (:87-88) */
+  return abi(amph_recombine_object((amph_ctx*)ctx, shares, n, lens, out, g_io, NULL));
 }
 
 int amphj_verify(void* ctx, const uint8_t* const* a, const size_t* lens, int64_t* fail) {
@@ -141,8 +156,7 @@ int amphj_verify_message(void* ctx, const uint8_t* y, const uint8_t* r, const ui
 }
 
 static int text_structs(int n, const char* const* texts, const size_t* lens, amph_odo_b64* odos) {
-  size_t W;
-  const int lst = odo_lengths(n, lens, &W);
+  const int lst = text_lengths(n, lens);
   if (lst) return lst;
   for (int j = 0; j < n; ++j) {
     odos[j].secret_shares = texts[0 * n + j];

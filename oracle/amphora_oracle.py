@@ -63,6 +63,27 @@ class IllegalArgumentException(ValueError):
     """java.lang.IllegalArgumentException as thrown on the path."""
 
 
+class ArrayIndexOutOfBoundsException(IndexError):
+    """java.lang.ArrayIndexOutOfBoundsException (Arrays.copyOfRange -> System.arraycopy)."""
+
+
+def copy_of_range(original: bytes, frm: int, to: int) -> bytes:
+    """java.util.Arrays.copyOfRange(byte[], from, to) (JDK 8-21): a new array
+    of to - from bytes holding original[from:min(len, to)] and zeros after
+    it; from > original.length throws ArrayIndexOutOfBoundsException (from ==
+    length is allowed and gives all zeros), from > to IllegalArgumentException.
+    recombineObject cuts every party's word with it (client
+    SecretShareUtil.java:87-88), which is what gives ragged party arrays
+    their meaning."""
+    if frm > to:
+        raise IllegalArgumentException("%d > %d" % (frm, to))
+    if frm < 0 or frm > len(original):
+        raise ArrayIndexOutOfBoundsException(
+            "arraycopy: source index %d out of bounds for byte[%d]" % (frm, len(original)))
+    part = bytes(original[frm:min(len(original), to)])
+    return part + bytes(to - frm - len(part))
+
+
 class MpSpdzIntegrationUtils:
     """Restatement of mp-spdz-integration 0.2.2 ``MpSpdzIntegrationUtils``.
 
@@ -122,7 +143,11 @@ class ClientSecretShareUtil:
         """recombineObject :70-90 with summingGfpAsBigInteger :53-63.
 
         The word count comes from ``shares.get(0).length / WORD_WIDTH`` (:75);
-        each word is the BigInteger sum of fromGfp over parties, then mod p."""
+        each party's word i is ``Arrays.copyOfRange(share, 16 i, 16 i + 16)``
+        (:87-88), so parties of other lengths than party 0 are cut, or
+        zero-padded past their end, or raise ArrayIndexOutOfBoundsException
+        for a word that starts past their end (``copy_of_range``); each word
+        is the BigInteger sum of fromGfp over parties, then mod p."""
         if len(shares) == 0:
             return []
         n_words = len(shares[0]) // WORD_WIDTH
@@ -130,7 +155,7 @@ class ClientSecretShareUtil:
         for i in range(n_words):
             acc = 0
             for s in shares:
-                acc += self.spdz.from_gfp(s[i * WORD_WIDTH:(i + 1) * WORD_WIDTH])
+                acc += self.spdz.from_gfp(copy_of_range(s, i * WORD_WIDTH, (i + 1) * WORD_WIDTH))
             out.append(acc % self.prime)
         return out
 

@@ -63,6 +63,24 @@ def default_threads() -> int:
     return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
 
 
+def java_words(buf, W: int):
+    """A party's byte[] as the W words recombineObject reads from it (client
+    SecretShareUtil.java:87-88): word i = Arrays.copyOfRange(buf, 16 i,
+    16 i + 16) -- amphora_oracle.copy_of_range, vectorised: cut past 16 W,
+    zero-padded past the end, ArrayIndexOutOfBoundsException when some word
+    i < W starts past the end (16 i > len).  Returns a (W, 16) uint8 array."""
+    from oracle.amphora_oracle import ArrayIndexOutOfBoundsException
+    a = np.frombuffer(bytes(buf), np.uint8) if isinstance(buf, (bytes, bytearray)) else \
+        np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+    if W and 16 * (W - 1) > a.size:
+        raise ArrayIndexOutOfBoundsException(
+            "arraycopy: word %d starts past the end of byte[%d]" % (a.size // 16 + 1, a.size))
+    out = np.zeros((W, 16), np.uint8)
+    k = min(a.size, 16 * W)
+    out.reshape(-1)[:k] = a[:k]
+    return out
+
+
 class Field:
     """One prime field; mirrors MpSpdzIntegrationUtils.of(prime, r, rInv)."""
 
@@ -107,6 +125,37 @@ class Field:
                                   np.ascontiguousarray(secrets16).ctypes.data, W,
                                   out.ctypes.data, self.threads)
         return out, ff
+
+    # -- recombineObject over parties of their own lengths ---------------------
+    def recombine_object(self, shares):
+        """recombineObject (SecretShareUtil.java:70-90): W = party 0's length
+        // 16, every party's words read as java_words does."""
+        if len(shares) == 0:
+            return np.empty((0, 16), np.uint8)
+        W = len(bytes(shares[0])) // 16 if isinstance(shares[0], (bytes, bytearray)) else \
+            np.asarray(shares[0]).nbytes // 16
+        return self.recombine([java_words(s, W) for s in shares])
+
+    def _java_odos(self, odos):
+        W = np.asarray(odos[0][0]).nbytes // 16
+        return [tuple(java_words(f, W) for f in o) for o in odos], W
+
+    def recombine_verify_object(self, odos):
+        """verifyOutputDeliveryObjects (DefaultAmphoraClient.java:476-505) over
+        byte[] fields of any length: the five recombineObject calls take
+        party 0's word count and copyOfRange semantics."""
+        jo, _ = self._java_odos(odos)
+        return self.recombine_verify(jo)
+
+    def mask_input_object(self, secrets16, mask_odos):
+        """createSecret (:150-160) over byte[] mask fields of any length:
+        verify every mask word, mask the len(secrets16) <= W first ones.
+        Returns (masked, first failing mask index or -1)."""
+        jo, W = self._java_odos(mask_odos)
+        _, ff = self.recombine_verify(jo)
+        S = secrets16.shape[0]
+        m, _ = self.mask_input(secrets16, [tuple(f[:S] for f in o) for o in jo])
+        return m, ff
 
     # -- service -----------------------------------------------------------
     def convert_share(self, masked16, tuples32, mac_key: int, use_zero_input: bool):

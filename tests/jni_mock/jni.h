@@ -8,8 +8,9 @@
  * other JNI function is called inside a Get/ReleasePrimitiveArrayCritical
  * region, that at most 16 local references (or what EnsureLocalCapacity
  * reserved) are live in one native call, and lets a test make a pin fail.
- * The JavaVM half (GetEnv / AttachCurrentThreadAsDaemon) lets the region-copy
- * callbacks run on libamphora_hip's staging threads, which attach as daemons.
+ * The JavaVM half (GetEnv / AttachCurrentThreadAsDaemon / DetachCurrentThread)
+ * lets the region-copy callbacks run on libamphora_hip's staging threads, which
+ * attach as daemons and must detach before they exit.
  * The real build (jni/Makefile) uses $JAVA_HOME/include/jni.h.
  */
 #ifndef JNI_MOCK_H_
@@ -48,6 +49,7 @@ typedef const struct JNIInvokeInterface_* JavaVM;
 struct JNIInvokeInterface_ {
   jint (*GetEnv)(JavaVM*, void**, jint);
   jint (*AttachCurrentThreadAsDaemon)(JavaVM*, void**, void*);
+  jint (*DetachCurrentThread)(JavaVM*);
 };
 
 struct JNINativeInterface_ {

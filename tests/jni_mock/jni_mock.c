@@ -37,6 +37,8 @@ static int g_pins;           /* critical pins taken since mock_clear */
 /* region-copy callbacks run on the library's staging threads: atomics */
 static long g_region_copies; /* Get/SetByteArrayRegion calls since mock_clear */
 static int g_attaches;       /* threads attached to the mock VM */
+static int g_detaches;       /* ... and detached again (at their exit) */
+static int g_bad_detaches;   /* DetachCurrentThread on the calling "Java" thread */
 static int g_global_refs;    /* live global references */
 static int g_foreign_regions; /* region copies made on threads other than mock_env()'s */
 static __thread int t_attached;
@@ -235,7 +237,16 @@ static const struct JNINativeInterface_ g_table = {
     m_EnsureLocalCapacity, m_GetJavaVM,        m_NewGlobalRef,       m_DeleteGlobalRef,
     m_ExceptionCheck,     m_ExceptionClear,
 };
-static const struct JNIInvokeInterface_ g_vm_table = {vm_GetEnv, vm_AttachCurrentThreadAsDaemon};
+static jint vm_DetachCurrentThread(JavaVM* vm) {
+  (void)vm;
+  if (t_attached == 1) __atomic_fetch_add(&g_bad_detaches, 1, __ATOMIC_RELAXED); /* the Java thread itself */
+  if (t_attached == 2) __atomic_fetch_add(&g_detaches, 1, __ATOMIC_RELAXED);
+  t_attached = 0;
+  return JNI_OK;
+}
+
+static const struct JNIInvokeInterface_ g_vm_table = {vm_GetEnv, vm_AttachCurrentThreadAsDaemon,
+                                                      vm_DetachCurrentThread};
 static JNIEnv g_env = &g_table;
 static JavaVM g_vm = &g_vm_table;
 
@@ -277,6 +288,8 @@ JNIEXPORT int mock_pins(void) { return g_pins; }
 JNIEXPORT long mock_region_copies(void) { return __atomic_load_n(&g_region_copies, __ATOMIC_RELAXED); }
 JNIEXPORT int mock_foreign_regions(void) { return __atomic_load_n(&g_foreign_regions, __ATOMIC_RELAXED); }
 JNIEXPORT int mock_attaches(void) { return __atomic_load_n(&g_attaches, __ATOMIC_RELAXED); }
+JNIEXPORT int mock_detaches(void) { return __atomic_load_n(&g_detaches, __ATOMIC_RELAXED); }
+JNIEXPORT int mock_bad_detaches(void) { return __atomic_load_n(&g_bad_detaches, __ATOMIC_RELAXED); }
 JNIEXPORT int mock_global_refs(void) { return __atomic_load_n(&g_global_refs, __ATOMIC_RELAXED); }
 
 JNIEXPORT void mock_clear(void) {

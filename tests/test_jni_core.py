@@ -107,6 +107,7 @@ def test_exception_mapping(J):
     assert J.amphj_exception_class(1) == b"io/carbynestack/amphora/common/exceptions/IntegrityVerificationException"
     assert J.amphj_exception_class(2) == J.amphj_exception_class(3) == IAE.encode()
     assert J.amphj_exception_class(4) == J.amphj_exception_class(5) == b"java/lang/IllegalStateException"
+    assert J.amphj_exception_class(6) == b"java/lang/ArrayIndexOutOfBoundsException"
 
 
 def test_checks_fire_before_the_abi(J):
@@ -490,3 +491,80 @@ def test_small_calls_still_pin(J, jctx, F, monkeypatch):
     assert e.call(CLIENT + "recombineVerify", C.c_int64, C.c_int64(jctx), *e.odo_lists(odos), out) == -1
     assert e.read(out) == F.recombine_verify(odos)[0].tobytes()
     assert J.mock_pins() == 11 and J.mock_region_copies() == 0 and e.clean()
+
+
+# ---- recombineObject's ragged party arrays through JNI (SecretShareUtil.java:70-90)
+AIOOBE = "java/lang/ArrayIndexOutOfBoundsException"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("region", [False, True])
+@pytest.mark.parametrize("delta,outcome", [(53, "ok"), (-8, "pad"), (-32, "range")])
+def test_client_ragged_partner(J, jctx, F, delta, outcome, region, monkeypatch):
+    """A partner whose ODO arrays are longer (cut), short by 8 bytes (last
+    word zero-padded: MAC failure at W-1, the padded word recombined) or
+    short by two words (ArrayIndexOutOfBoundsException), through
+    recombineVerify, maskInput and recombine, pinned and region-copied --
+    each against the oracle's restatement of copyOfRange."""
+    from tests.test_ragged_parties import _ragged
+    from oracle import amphora_oracle as O
+    if region:
+        monkeypatch.setenv("AMPH_JNI_REGION_BYTES", "0")
+    else:
+        monkeypatch.delenv("AMPH_JNI_REGION_BYTES", raising=False)
+    e = Env(J)
+    ctx = C.c_int64(jctx)
+    W, n = 5000, 3
+    odos = _ragged(F, W, n, delta, seed=71)
+    secrets = F.synth_words(seed=72, count=W, mont=False)
+    J.mock_clear()
+    out = e.zeros(16 * W)
+    got = e.call(CLIENT + "recombineVerify", C.c_int64, ctx, *e.odo_lists(odos), out)
+    if outcome == "range":
+        assert got == -1 and e.exception()[0] == AIOOBE and e.clean()
+        with pytest.raises(O.ArrayIndexOutOfBoundsException):
+            F.recombine_verify_object(odos)
+        J.mock_clear()
+        e.call(CLIENT + "maskInput", C.c_int64, ctx, *e.odo_lists(odos), e.bytes(secrets), e.zeros(16 * W))
+        assert e.exception()[0] == AIOOBE and e.clean()
+        J.mock_clear()
+        e.call(CLIENT + "recombine", None, ctx, e.objects([e.bytes(o[0]) for o in odos]), e.zeros(16 * W))
+        assert e.exception()[0] == AIOOBE and e.clean()
+        return
+    ey, eff = F.recombine_verify_object(odos)
+    assert got == eff == (-1 if outcome == "ok" else W - 1)
+    assert e.exception() is None and e.clean() and e.read(out) == ey.tobytes()
+    out = e.zeros(16 * W)
+    em, mff = F.mask_input_object(secrets, odos)
+    assert e.call(CLIENT + "maskInput", C.c_int64, ctx, *e.odo_lists(odos), e.bytes(secrets), out) == mff
+    assert e.exception() is None and e.clean() and e.read(out) == em.tobytes()
+    out = e.zeros(16 * W)
+    e.call(CLIENT + "recombine", None, ctx, e.objects([e.bytes(o[4]) for o in odos]), out)
+    assert e.exception() is None and e.read(out) == F.recombine_object([o[4] for o in odos]).tobytes()
+    if region:
+        assert J.mock_pins() == 0
+
+
+@pytest.mark.gpu
+def test_staging_threads_detach_when_the_context_goes(J, F, monkeypatch):
+    """libamphora_hip's staging threads attach to the VM as daemons
+    for the region-copy callbacks; each must detach before it exits (JNI
+    spec).  A context of its own, large calls in region mode, then
+    ctxDestroy (which joins the threads): every attach is matched by a
+    detach, and the calling Java thread is never detached."""
+    monkeypatch.setenv("AMPH_JNI_REGION_BYTES", "0")
+    J.mock_detaches.restype = J.mock_bad_detaches.restype = C.c_int
+    a0, d0 = J.mock_attaches(), J.mock_detaches()
+    e = Env(J)
+    h = e.call(CLIENT + "ctxCreate", C.c_int64, e.bytes(le16(P)), e.bytes(le16(R)), e.bytes(le16(RINV)), None)
+    assert h != 0 and e.exception() is None
+    W, n = 300_000, 3
+    odos, _ = F.synth_odos(seed=91, n=n, W=W)
+    out = e.zeros(16 * W)
+    assert e.call(CLIENT + "recombineVerify", C.c_int64, C.c_int64(h), *e.odo_lists(odos), out) == -1
+    assert e.read(out) == F.recombine_verify(odos)[0].tobytes()
+    attached = J.mock_attaches() - a0
+    assert attached > 0, "the batched pipeline's staging threads ran the callbacks"
+    Env(J).call(CLIENT + "ctxDestroy", None, C.c_int64(h))
+    assert J.mock_detaches() - d0 == attached
+    assert J.mock_bad_detaches() == 0

@@ -445,3 +445,42 @@ def max_pooled_estimate(pooled, sizes):
     """Bytes of the largest pooled session buffer: sizes double, so it is
     W_max / sum(W) of the pooled bytes."""
     return pooled * sizes[-1] // sum(sizes)
+
+
+def test_session_device_mode_keeps_its_own_verdicts(ctx, F):
+    """the partner verdict finish_b64_dev checks is the session's
+    own copy, taken on the partner call's stream, and finish waits for that
+    call's work even on another stream.  So after the partner call the caller
+    may overwrite its bad_index word: a rejected text still poisons the
+    fields, an accepted one is not poisoned by a later write into the word."""
+    import torch
+    n, W = 2, 3000
+    shares, masks, triples = party_inputs(F, n, W)
+    pre = [F.odo_pre(shares[j], 32, masks[j], triples[j]) for j in range(n)]
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    t1 = ctx.party_begin(shares[1], 32, masks[1], triples[1], n).text()
+    at = t1.index(b":") + 3
+    bad_text = dev(np.frombuffer(t1[:at] + b"x" + t1[at + 1:], np.uint8).copy())
+    good_text = dev(np.frombuffer(t1, np.uint8).copy())
+    opened = F.recombine_diffs([pre[0][3], pre[1][3]], [pre[0][4], pre[1][4]])
+    ow, ou = F.odo_post(opened, triples[0], True)
+    want = [base64.b64encode(x.tobytes()) for x in (pre[0][0], pre[0][1], pre[0][2], ow, ou)]
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    for text, poisoned in ((bad_text, True), (good_text, False)):
+        torch.cuda.synchronize()
+        s = ctx.party_begin_dev(dev(shares[0]), 32, dev(masks[0]), dev(triples[0]), n)
+        torch.cuda.synchronize()
+        word = torch.empty(1, dtype=torch.int64, device="cuda")
+        with torch.cuda.stream(sa):
+            s.partner(1, text, bad=word)
+            # the caller reuses its word right after the call (same stream)
+            word.fill_(0x7F7F7F7F7F7F7F7F if poisoned else 5)
+        with torch.cuda.stream(sb):
+            fields = s.finish_b64(True)
+        torch.cuda.synchronize()
+        got = [f.cpu().numpy().tobytes() for f in fields]
+        if poisoned:
+            assert all(g[:4] == b"!!!!" for g in got)
+        else:
+            assert got == want
+        s.close()
