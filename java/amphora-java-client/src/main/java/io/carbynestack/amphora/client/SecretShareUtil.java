@@ -80,7 +80,12 @@ class SecretShareUtil implements AutoCloseable {
     return MaskedInputData.of(NativeShareArithmetic.maskWord(ctx, s, m));
   }
 
-  /** recombineObject :70-90: word i = sum over the shares of fromGfp(word i) mod p */
+  /**
+   * recombineObject :70-90: word i = sum over the shares of fromGfp(word i) mod p. The word count
+   * is shares.get(0).length / 16 and the other parties' arrays keep the reference's
+   * Arrays.copyOfRange semantics (longer: cut; ending inside the last word: zero-padded; shorter
+   * than that: ArrayIndexOutOfBoundsException) -- amph_recombine_object, INTEGRATION.md.
+   */
   List<BigInteger> recombineObject(List<byte[]> shares) {
     if (shares.isEmpty()) {
       return new ArrayList<>();
