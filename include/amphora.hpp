@@ -18,6 +18,7 @@
 #ifndef AMPHORA_HPP_
 #define AMPHORA_HPP_
 
+#include <algorithm>
 #include <array>
 #include <cmath>
 #include <cstdint>
@@ -52,9 +53,24 @@ struct NativeError : std::runtime_error {
   int status;
   NativeError(int st, const std::string& m) : std::runtime_error(m), status(st) {}
 };
+// java.lang.ArrayIndexOutOfBoundsException: a ragged party's word starts past
+// its array's end (recombineObject's Arrays.copyOfRange, AMPH_E_RANGE)
+struct ArrayIndexOutOfBoundsException : std::out_of_range {
+  using std::out_of_range::out_of_range;
+};
 
 inline void check(int st) {
+  if (st == AMPH_E_RANGE) throw ArrayIndexOutOfBoundsException(amph_last_error());
   if (st != AMPH_OK) throw NativeError(st, std::string(amph_strerror(st)) + ": " + amph_last_error());
+}
+
+// java.util.Arrays.copyOfRange(byte[], from, to): zero-padded past the end,
+// ArrayIndexOutOfBoundsException when `from` is past it
+inline std::vector<uint8_t> copyOfRange(const std::vector<uint8_t>& a, size_t from, size_t to) {
+  if (from > a.size()) throw ArrayIndexOutOfBoundsException("copyOfRange: from past the end of the array");
+  std::vector<uint8_t> out(to - from, 0);
+  std::copy(a.begin() + from, a.begin() + std::min(a.size(), to), out.begin());
+  return out;
 }
 
 inline void storeLe(u128 x, uint8_t* out) {
@@ -183,17 +199,18 @@ class SecretShareUtil {
     return out;
   }
 
-  // recombineObject :70-90
+  // recombineObject :70-90 (parties of their own lengths: copyOfRange semantics,
+  // ArrayIndexOutOfBoundsException for a word past a shorter party's end)
   std::vector<u128> recombineObject(const std::vector<Bytes>& shares) const {
     if (shares.empty()) return {};
     std::vector<const uint8_t*> ptrs;
+    std::vector<size_t> lens;
     for (auto& s : shares) {
-      if (s.size() / 16 < shares[0].size() / 16) throw std::out_of_range("share arrays shorter than the first");
       ptrs.push_back(s.data());
+      lens.push_back(s.size());
     }
-    const size_t nb = shares[0].size() / 16 * 16;
-    Bytes out(nb);
-    check(amph_recombine(ctx_.get(), ptrs.data(), (int)ptrs.size(), nb, out.data(), 0, nullptr));
+    Bytes out(shares[0].size() / 16 * 16);
+    check(amph_recombine_object(ctx_.get(), ptrs.data(), (int)ptrs.size(), lens.data(), out.data(), 0, nullptr));
     return unpackWords(out);
   }
 
@@ -261,7 +278,7 @@ inline std::vector<u128> verifyOutputDeliveryObjects(const SecretShareUtil& util
       for (auto& o : odos) {
         const Bytes& src = k == 0 ? o.getSecretShares() : k == 1 ? o.getRShares() : k == 2 ? o.getVShares()
                          : k == 3 ? o.getWShares() : o.getUShares();
-        sh.emplace_back(src.begin() + 16 * ff, src.begin() + 16 * ff + 16);
+        sh.push_back(copyOfRange(src, 16 * ff, 16 * ff + 16));  // a ragged party's word: zero-padded
       }
       f[k] = util.recombineObject(sh);
     }

@@ -281,12 +281,68 @@ static void gpu_tests() {
   EXPECT(threw);
 }
 
+// recombineObject's ragged partner arrays (SecretShareUtil.java:75,87-88) through
+// the mirror: longer -> cut; 8 bytes short -> last word zero-padded, MAC failure
+// at W-1 with the reference's message; two words short -> ArrayIndexOutOfBounds.
+static void ragged_tests(const client::SecretShareUtil& util) {
+  const Context& c = util.context();
+  const size_t W = 6;
+  std::vector<u128> ys, rs, vs;
+  std::mt19937_64 rng(7);
+  for (size_t i = 0; i < W; ++i) {  // 63-bit values: the products stay below p
+    ys.push_back((u128)(rng() >> 1));
+    rs.push_back((u128)(rng() >> 1));
+    vs.push_back((u128)(rng() >> 1));
+  }
+  auto prod = [&](const std::vector<u128>& a, const std::vector<u128>& b) {
+    std::vector<u128> o;
+    for (size_t i = 0; i < a.size(); ++i) o.push_back(a[i] * b[i]);
+    return o;
+  };
+  const std::vector<u128> ws = prod(ys, rs), us = prod(vs, rs);
+  // party 0 holds the values, party 1 zeros: shares of honest words
+  const std::vector<u128> zero(W, 0);
+  auto odo = [&](const std::vector<u128>& y, const std::vector<u128>& r, const std::vector<u128>& v,
+                 const std::vector<u128>& w, const std::vector<u128>& u, long delta) {
+    Bytes f[5] = {c.toGfp(y), c.toGfp(r), c.toGfp(v), c.toGfp(w), c.toGfp(u)};
+    for (auto& b : f) b.resize((size_t)((long)b.size() + delta), 0x5A);
+    return OutputDeliveryObject(f[0], f[1], f[2], f[3], f[4]);
+  };
+  const OutputDeliveryObject p0 = odo(ys, rs, vs, ws, us, 0);
+  EXPECT(client::verifyOutputDeliveryObjects(util, {p0, odo(zero, zero, zero, zero, zero, 40)}) == ys);
+  bool threw = false;
+  try {
+    client::verifyOutputDeliveryObjects(util, {p0, odo(zero, zero, zero, zero, zero, -8)});
+  } catch (const IntegrityVerificationException& e) {
+    threw = std::string(e.what()).rfind("Verification of secret has failed:", 0) == 0;
+  }
+  EXPECT(threw);
+  threw = false;
+  try {
+    client::verifyOutputDeliveryObjects(util, {p0, odo(zero, zero, zero, zero, zero, -32)});
+  } catch (const ArrayIndexOutOfBoundsException&) {
+    threw = true;
+  }
+  EXPECT(threw);
+  Bytes a = c.toGfp(ys), b(16 * W - 8, 0);
+  EXPECT(util.recombineObject({a, b}) == ys);  // zero shares, zero padding: the values themselves
+  threw = false;
+  try {
+    util.recombineObject({a, Bytes(16 * W - 17, 0)});
+  } catch (const ArrayIndexOutOfBoundsException&) {
+    threw = true;
+  }
+  EXPECT(threw);
+  EXPECT(copyOfRange(Bytes{1, 2, 3}, 2, 6) == (Bytes{3, 0, 0, 0}));
+}
+
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "cpu";
   try {
     cpu_tests();
     if (mode == "gpu") {
       gpu_tests();
+      ragged_tests(client::SecretShareUtil::of(P, R, RI));
       Context c(P, R, RI);
       kat2_service(c);
     }
