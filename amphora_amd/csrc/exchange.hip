@@ -24,8 +24,9 @@
 // validated without a second pass; the first malformed byte's offset is
 // reported.  Whitespace between tokens is accepted, as in any JSON reader.
 //
-// Decimal conversion: 128-bit magnitude <-> five base-10^9 chunks (nine
-// 64-by-32-bit divisions by a constant in all, to_chunks), chunks <-> digits.
+// Decimal conversion: 128-bit magnitude <-> five base-10^9 chunks (a
+// multiply-accumulate over the limbs with four carry divisions by a constant,
+// to_chunks), chunks <-> digits.
 #include <hip/hip_ext.h>
 
 #include <algorithm>
@@ -74,35 +75,42 @@ __device__ __forceinline__ uint32_t div_step_e9(uint64_t& rem, uint32_t x) {
 }
 
 // 128-bit magnitude -> base-10^9 chunks (little end first); returns the
-// decimal digit count (1 for zero).  Any x < 2^128 leaves x / 10^9 < 2^98.1,
-// x / 10^18 < 2^68.2, x / 10^27 < 2^38.3 and x / 10^36 < 2^8.4, so after
-// each round the leading limb is known to be below 10^9 (it becomes the
-// next round's starting remainder with no division) and one more limb is
-// zero: 9 64-bit divisions + 1 32-bit one instead of 5 rounds x 4.
+// decimal digit count (1 for zero).  Multiply-accumulate form: with the limbs
+// x_i of x = sum x_i 2^(32 i) and the base-10^9 digits of 2^32, 2^64, 2^96
+//   2^32 = 4 | 294967296,  2^64 = 18 | 446744073 | 709551616,
+//   2^96 = 79 | 228162514 | 264337593 | 543950336,
+// column k of the base-10^9 product sum is A_k = carry + sum x_i c_(i,k):
+// nine v_mad_u64_u32 and one carry division per column (ten 64-by-32-bit
+// division steps by a constant became four: 12 % fewer VALU in k_xenc_write).
+// Bounds (x_i < 2^32): A_0 < 6.7e18 (its high word can reach 1.55e9, so one
+// 32-bit division takes it below 10^9 first), A_1 < 3.1e18, A_2 < 1e18,
+// A_3 < 3.5e11 -- each high word < 10^9, as div_step_e9 requires, and every
+// quotient < 2^32 except A_0's (< 2^33, kept as qa:q0).
+__device__ __forceinline__ uint64_t mad_u64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
+
 __device__ __forceinline__ int to_chunks(const uint4& m, uint32_t (&ch)[5]) {
-  uint64_t rem = 0;
-  const uint32_t a3 = m.w / (uint32_t)kE9;  // < 5
-  rem = m.w - a3 * (uint32_t)kE9;
-  const uint32_t a2 = div_step_e9(rem, m.z), a1 = div_step_e9(rem, m.y);
-  const uint32_t a0 = div_step_e9(rem, m.x);
+  uint64_t A = mad_u64(m.w, 543950336u, mad_u64(m.z, 709551616u, mad_u64(m.y, 294967296u, m.x)));
+  const uint32_t ah = (uint32_t)(A >> 32), qa = ah / (uint32_t)kE9;  // qa <= 1
+  uint64_t rem = ah - qa * (uint32_t)kE9;
+  const uint64_t q0 = ((uint64_t)qa << 32) | div_step_e9(rem, (uint32_t)A);
   ch[0] = (uint32_t)rem;
-  rem = a3;  // x / 10^9 = (a3, a2, a1, a0) < 2^98.1
-  const uint32_t b2 = div_step_e9(rem, a2), b1 = div_step_e9(rem, a1);
-  const uint32_t b0 = div_step_e9(rem, a0);
+  A = mad_u64(m.w, 264337593u, mad_u64(m.z, 446744073u, mad_u64(m.y, 4u, q0)));
+  rem = A >> 32;
+  const uint32_t q1 = div_step_e9(rem, (uint32_t)A);
   ch[1] = (uint32_t)rem;
-  rem = b2;  // x / 10^18 = (b2, b1, b0) < 2^68.2
-  const uint32_t c1 = div_step_e9(rem, b1), c0 = div_step_e9(rem, b0);
+  A = mad_u64(m.w, 228162514u, mad_u64(m.z, 18u, q1));
+  rem = A >> 32;
+  const uint32_t q2 = div_step_e9(rem, (uint32_t)A);
   ch[2] = (uint32_t)rem;
-  rem = c1;  // x / 10^27 = (c1, c0) < 2^38.3
-  const uint32_t d0 = div_step_e9(rem, c0);
+  A = mad_u64(m.w, 79u, q2);
+  rem = A >> 32;
+  ch[4] = div_step_e9(rem, (uint32_t)A);  // x / 10^36 < 2^8.4
   ch[3] = (uint32_t)rem;
-  ch[4] = d0;  // x / 10^36 < 2^8.4
   int top = 0;
 #pragma unroll
   for (int k = 1; k < 5; ++k) top = ch[k] ? k : top;
   return 9 * top + ndigits32(ch[top]);
 }
-
 
 __device__ __forceinline__ char* put_str(char* o, const char* s) {
   while (*s) *o++ = *s++;

@@ -300,26 +300,39 @@ static void ragged_tests(const client::SecretShareUtil& util) {
     return o;
   };
   const std::vector<u128> ws = prod(ys, rs), us = prod(vs, rs);
-  // party 0 holds the values, party 1 zeros: shares of honest words
-  const std::vector<u128> zero(W, 0);
+  // honest 2-party shares: party 1 random, party 0 the difference mod p
+  auto subMod = [](u128 a, u128 b) { return a >= b ? a - b : a + (P - b); };
+  auto share1 = [&]() {
+    std::vector<u128> o;
+    for (size_t i = 0; i < W; ++i) o.push_back((((u128)rng() << 64) | rng()) % P);
+    return o;
+  };
+  auto minus = [&](const std::vector<u128>& a, const std::vector<u128>& b) {
+    std::vector<u128> o;
+    for (size_t i = 0; i < a.size(); ++i) o.push_back(subMod(a[i], b[i]));
+    return o;
+  };
+  const std::vector<u128> y1 = share1(), r1 = share1(), v1 = share1(), w1 = share1(), u1 = share1();
   auto odo = [&](const std::vector<u128>& y, const std::vector<u128>& r, const std::vector<u128>& v,
                  const std::vector<u128>& w, const std::vector<u128>& u, long delta) {
     Bytes f[5] = {c.toGfp(y), c.toGfp(r), c.toGfp(v), c.toGfp(w), c.toGfp(u)};
     for (auto& b : f) b.resize((size_t)((long)b.size() + delta), 0x5A);
     return OutputDeliveryObject(f[0], f[1], f[2], f[3], f[4]);
   };
-  const OutputDeliveryObject p0 = odo(ys, rs, vs, ws, us, 0);
-  EXPECT(client::verifyOutputDeliveryObjects(util, {p0, odo(zero, zero, zero, zero, zero, 40)}) == ys);
+  const OutputDeliveryObject p0 = odo(minus(ys, y1), minus(rs, r1), minus(vs, v1), minus(ws, w1), minus(us, u1), 0);
+  auto p1 = [&](long delta) { return odo(y1, r1, v1, w1, u1, delta); };
+  EXPECT(client::verifyOutputDeliveryObjects(util, {p0, p1(0)}) == ys);
+  EXPECT(client::verifyOutputDeliveryObjects(util, {p0, p1(40)}) == ys);  // longer: cut
   bool threw = false;
-  try {
-    client::verifyOutputDeliveryObjects(util, {p0, odo(zero, zero, zero, zero, zero, -8)});
+  try {  // 8 bytes short: the last word zero-padded, its MAC check fails
+    client::verifyOutputDeliveryObjects(util, {p0, p1(-8)});
   } catch (const IntegrityVerificationException& e) {
     threw = std::string(e.what()).rfind("Verification of secret has failed:", 0) == 0;
   }
   EXPECT(threw);
   threw = false;
   try {
-    client::verifyOutputDeliveryObjects(util, {p0, odo(zero, zero, zero, zero, zero, -32)});
+    client::verifyOutputDeliveryObjects(util, {p0, p1(-32)});
   } catch (const ArrayIndexOutOfBoundsException&) {
     threw = true;
   }

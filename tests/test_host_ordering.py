@@ -2,9 +2,13 @@
 hipMemcpyAsync only with page-locked host memory; pageable memory moves with
 a blocking hipMemcpy once the context stream is idle.
 
-* CPU: a static check of capi.hip -- every hipMemcpyAsync sits in the batched
-  pipeline (run_batched_impl), whose host operands are page-locked (the
-  caller's registered buffer, or the slot's pinned staging buffer).
+* CPU: a static check of capi.hip -- every hipMemcpyAsync with a host
+  operand sits in the batched pipeline (run_batched_impl), whose host
+  operands are page-locked (the caller's registered buffer, or the slot's
+  pinned staging buffer); device-to-device async copies and stream-ordered
+  allocations appear only in device-mode code (the ragged-party tail of
+  ragged_odo_call / amph_recombine_object, which stages one word per party
+  on the caller's stream).
 * GPU: a FRESH process's first calls -- the situation in which round 2 saw
   a pageable async copy arrive after the kernel that read it -- through the
   wire-text K_RV (text staged from pageable memory), the base64 decode with a
@@ -40,18 +44,27 @@ def test_async_copies_only_in_the_pinned_pipeline():
     src = open(CAPI).read()
     code = re.sub(r"//[^\n]*", "", src)  # comments may name the call
     spans = _function_spans(code)
-    calls = [m.start() for m in re.finditer(r"\bhipMemcpy(?:2D)?Async\s*\(", code)]
+    calls = [m for m in re.finditer(r"\bhipMemcpy(?:2D)?Async\s*\(([^;]*)\);", code)]
     assert calls, "expected the batched pipeline's copies"
-    for pos in calls:
-        owner = [n for n, a, b in spans if a <= pos <= b]
+    device_only = ("stage_tail", "ragged_odo_call", "amph_recombine_object", "amph_party_partner_dev")
+    for m in calls:
+        owner = [n for n, a, b in spans if a <= m.start() <= b]
+        if "hipMemcpyDeviceToDevice" in m.group(1):  # no host operand
+            assert owner and owner[-1] in device_only, (m.group(0), owner)
+            continue
         assert owner and owner[-1] == "run_batched_impl", \
-            "hipMemcpyAsync outside the page-locked pipeline at offset %d (%s)" % (pos, owner)
+            "hipMemcpyAsync outside the page-locked pipeline at offset %d (%s)" % (m.start(), owner)
     body = next(code[a:b] for n, a, b in spans if n == "run_batched_impl")
     # host operands: the caller's buffer only when it is page-locked, else the slot's pinned
     # buffer (always for AMPH_F_HOST_IO arrays, which are callbacks, not memory)
     assert "in_pinned[k] = !ins[k].io && amph::is_pinned_host(ins[k].host)" in body
     assert "out_pinned[k] = !outs[k].io && amph::is_pinned_host(outs[k].host)" in body
-    assert "hipMallocAsync" not in code, "stream-ordered staging is not used for host calls"
+    # stream-ordered allocation: only the device-mode ragged tail's one-word staging
+    for m in re.finditer(r"\bhipMallocAsync\s*\(", code):
+        owner = [n for n, a, b in spans if a <= m.start() <= b]
+        assert owner and owner[-1] in ("ragged_odo_call", "amph_recombine_object"), owner
+        body = next(code[a:b] for n, a, b in spans if n == owner[-1])
+        assert "AMPH_F_DEVICE" in body[:body.find("hipMallocAsync")], "device-mode branch only"
 
 
 _FIRST_CALL = r"""
