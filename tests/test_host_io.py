@@ -128,3 +128,38 @@ def test_ragged_parties_host_io(env, delta, outcome):
     assert np.array_equal(ho.arr.reshape(W, 16), F.recombine_object([o[2] for o in odos]))
     for d in [x for ds in descs for x in ds] + [out, hs, hm, ho]:
         assert d.out_of_range == 0, "a callback was asked for bytes past its array's end"
+
+
+def test_failed_callback_leaves_nothing_in_flight(env):
+    """a read callback that fails part-way through a batched call
+    (batches before it already copied in, their kernels and copies out
+    queued) makes the call return AMPH_E_PARAM only after the pipeline's
+    streams have drained (run_batched synchronises them on every error), so
+    the next call -- which reuses the same page-locked staging slots -- gets
+    exact results."""
+    A, ctx, F = env
+    W, n = 1 << 20, 2
+    odos, _ = F.synth_odos(seed=41, n=n, W=W)
+    good = [[HostArray(f) for f in o] for o in odos]
+    lens = [o[0].nbytes for o in odos]
+    bad = [[HostArray(f) for f in o] for o in odos]
+    calls = {"n": 0}
+    orig = bad[1][3]._rd
+
+    def flaky(a, off, nb, dst):  # party 1's w field: the 3rd read fails
+        calls["n"] += 1
+        return -1 if calls["n"] == 3 else orig(a, off, nb, dst)
+    bad[1][3]._rd2 = RW(flaky)
+    bad[1][3].desc = _Desc(bad[1][3]._rd2, bad[1][3]._wr, None)
+    out = HostArray(np.zeros((W, 16), np.uint8))
+    ff = C.c_int64(-1)
+    st = A._lib.lib.amph_recombine_verify(ctx._h, _odo_array(A, bad, lens, n), n, out.ptr, C.byref(ff),
+                                          AMPH_F_HOST_IO, None)
+    assert st == A._lib.AMPH_E_PARAM and calls["n"] >= 3
+    out2 = HostArray(np.zeros((W, 16), np.uint8))
+    ff = C.c_int64(-1)
+    st = A._lib.lib.amph_recombine_verify(ctx._h, _odo_array(A, good, lens, n), n, out2.ptr, C.byref(ff),
+                                          AMPH_F_HOST_IO, None)
+    ey, eff = F.recombine_verify(odos)
+    assert st == 0 and ff.value == eff == -1
+    assert np.array_equal(out2.arr.reshape(W, 16), ey)
