@@ -409,9 +409,9 @@ def host_memory_phase(a, torch, dist, ctx, rank, world, distributed):
         ctx.set_batch_words(a.batch_words)
         odos = [tuple(odos_h[k, j] for k in range(5)) for j in range(n)]
         # the link itself, same arrays: pinned HtoD / DtoH copies on one stream
-        probe_dev = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
-        src = torch.from_numpy(odos_h.reshape(-1)[:1 << 30])
+        src = torch.from_numpy(odos_h.reshape(-1)[:min(1 << 30, odos_h.nbytes)])
         dst = torch.from_numpy(masked_h.reshape(-1)[:min(1 << 29, masked_h.nbytes)])
+        probe_dev = torch.empty(src.numel(), dtype=torch.uint8, device="cuda")
 
         def copy_rate(fn, nbytes, reps=3):
             fn()
@@ -475,8 +475,8 @@ def host_memory_phase(a, torch, dist, ctx, rank, world, distributed):
                 "host_GBps": (htod_b + dtoh_b) * W * world * a.host_steps / el / 1e9,
                 "htod_GBps_per_rank": round(htod, 2),
                 "link_probe_GBps": {"htod": round(htod_link, 2), "dtoh": round(dtoh_link, 2),
-                                    "note": "pinned copies of 1 GiB / 512 MiB of the same arrays, "
-                                            "min over ranks"},
+                                    "bytes": [int(src.numel()), int(dst.numel())],
+                                    "note": "pinned copies of the same arrays (HtoD, DtoH bytes), min over ranks"},
                 "frac_of_link": round(htod / htod_link, 4),
                 "memory": "page-locked caller arrays (amph_host_register), outputs reused across calls",
                 "workload": "C5 per-GPU share: amph_mask_input + amph_recombine_verify from host "
