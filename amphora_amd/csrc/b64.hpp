@@ -190,4 +190,49 @@ __device__ __forceinline__ void enc_word24(const uint4 v, uint32_t (&g)[6]) {
   g[5] = (enc_group_w<5>(w) & 0xFFFFu) | ((uint32_t)'=' << 16) | ((uint32_t)'=' << 24);
 }
 
+
+// ---- base64 decode through an LDS table (wire kernels' fast path) -------------
+// kB64Val[c] = the 6-bit value of base64 character c, 0x80 for any other byte.
+struct B64ValTable {
+  uint8_t v[256];
+  constexpr B64ValTable() : v() {
+    for (int c = 0; c < 256; ++c) v[c] = 0x80;
+    for (int c = 'A'; c <= 'Z'; ++c) v[c] = (uint8_t)(c - 'A');
+    for (int c = 'a'; c <= 'z'; ++c) v[c] = (uint8_t)(c - 'a' + 26);
+    for (int c = '0'; c <= '9'; ++c) v[c] = (uint8_t)(c - '0' + 52);
+    v['+'] = 62;
+    v['/'] = 63;
+  }
+};
+__device__ constexpr B64ValTable kB64Val{};
+// One byte per entry: the 256-byte table spans the 64 LDS banks once, so two
+// lookups either share a dword (a broadcast) or sit in different banks.  A 4-byte
+// stride (one bank per character) measured slower: profiles/r05_wire_lut_ab.txt.
+constexpr int kLutBytes = 256;
+
+// Fill the workgroup's LDS copy, any block size (the caller synchronises).
+__device__ __forceinline__ void b64_lut_fill(uint8_t* lut) {
+  for (uint32_t c = threadIdx.x; c < 256; c += blockDim.x) lut[c] = kB64Val.v[c];
+}
+
+// One 16-character unit through the table: 16 lookups, each group's 24 bits
+// as (v0 << 18) | (v1 << 12) | (v2 << 6) | v3, the 12 bytes by three
+// v_perm_b32 as dec_unit16_ok; the OR of the 16 table values accumulates into
+// bad (bit 7 set iff a character outside the alphabet was seen).
+__device__ __forceinline__ void dec_unit16_lut(const uint4 v, uint32_t (&o)[3], uint32_t& bad, const uint8_t* lut) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t g[4], acc = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t a = lut[w[q] & 0xFFu], b = lut[(w[q] >> 8) & 0xFFu];
+    const uint32_t c = lut[(w[q] >> 16) & 0xFFu], d = lut[w[q] >> 24];
+    acc |= a | b | c | d;
+    g[q] = (((((a << 6) | b) << 6) | c) << 6) | d;
+  }
+  bad |= acc;
+  o[0] = __builtin_amdgcn_perm(g[1], g[0], 0x06000102u);
+  o[1] = __builtin_amdgcn_perm(g[2], g[1], 0x05060001u);
+  o[2] = __builtin_amdgcn_perm(g[3], g[2], 0x04050600u);
+}
+
 }  // namespace amph

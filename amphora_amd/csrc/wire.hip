@@ -65,7 +65,7 @@ __device__ __forceinline__ uint32_t dec_unit_slow(const char* t, size_t unit, si
 // Fast-path loads: kWirePrefetch > 0 issues field f + kWirePrefetch's load
 // while field f is decoded (fewer live VGPRs); 0 issues all 5N up front.
 #ifndef AMPH_WIRE_PD
-#define AMPH_WIRE_PD 0
+#define AMPH_WIRE_PD 3  // with the LDS-table decode: 73-77 VGPRs at 3 parties (0: 99-101)
 #endif
 constexpr int kWirePrefetch = AMPH_WIRE_PD;
 
@@ -73,7 +73,10 @@ constexpr int kWirePrefetch = AMPH_WIRE_PD;
 // each barrier (2G buffers alternate, or all 5N at once, one barrier in all,
 // when G >= 5N).
 #ifndef AMPH_WIRE_G
-#define AMPH_WIRE_G 5  // 2-5 % over 1 at 1 and 16 Mi words (profiles/r02_ubench_wire_groups.txt)
+// 3: 6 buffers + the 256-byte decode table = 18.7 KB per block, so LDS allows
+// 6 waves per SIMD as the VGPRs do (G = 5: 30.3 KB, 5 waves); k_mask_b64
+// -5 % at 4 Mi x 3 (profiles/r05_wire_lut_ab.txt).  r02: G = 5 was 2-5 % over 1.
+#define AMPH_WIRE_G 3
 #endif
 template <int NP>
 struct WireGroups {
@@ -96,14 +99,14 @@ template <int NP, bool BIG, bool FAST, int BS>
 __device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nchars, uint32_t pad,
                                             size_t words, uint4 (&raw)[5][NP > 0 ? NP : 1],
                                             uint32_t (*lds)[3 * BS], W4 (&acc)[5],
-                                            unsigned long long* bad, const Fp& f, size_t tile) {
+                                            unsigned long long* bad, const Fp& f, size_t tile,
+                                            const uint8_t* lutp) {
   constexpr int G = WireGroups<NP>::G, NB = WireGroups<NP>::bufs;
   const size_t unit = tile * BS + threadIdx.x;
   const size_t word = tile * Wire<BS>::words + threadIdx.x;
   const bool consumer = threadIdx.x < Wire<BS>::words && word < words;
   const int np = NP > 0 ? NP : n;
   int slot = 0;  // LDS buffer of the next field
-  const DecTabs tabs = dec_tabs_vgpr();
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
 #pragma unroll
@@ -116,14 +119,14 @@ __device__ __forceinline__ void wire_fields(const TextSet& tx, int n, size_t nch
           if (ahead < 5 * NP)
             raw[ahead / NP][ahead % NP] = ld(reinterpret_cast<const uint4*>(tx.t[ahead / NP][ahead % NP]) + unit);
         }
-        uint32_t ok = 0x80808080u;
-        dec_unit16_ok(raw[k][j], o, ok, tabs);
-        if (ok != 0x80808080u) bad_unit(raw[k][j], j, k, nchars, unit, bad);
+        uint32_t badb = 0;  // the per-unit branch also bounds the LDS reads' live ranges: one
+        dec_unit16_lut(raw[k][j], o, badb, lutp);  // check after the last field took 117-256 VGPRs
+        if (badb & 0x80u) bad_unit(raw[k][j], j, k, nchars, unit, bad);
       } else if constexpr (FAST) {
         const uint4 v = ld(reinterpret_cast<const uint4*>(tx.t[k][j]) + unit);
-        uint32_t ok = 0x80808080u;
-        dec_unit16_ok(v, o, ok, tabs);
-        if (ok != 0x80808080u) bad_unit(v, j, k, nchars, unit, bad);
+        uint32_t badb = 0;
+        dec_unit16_lut(v, o, badb, lutp);
+        if (badb & 0x80u) bad_unit(v, j, k, nchars, unit, bad);
       } else {
         const uint32_t fb = dec_unit_slow(tx.t[k][j], unit, nchars, pad, o);
         if (fb != 0xFFFFFFFFu)  // (party j, field k) in ODO order, then the offset
@@ -233,14 +236,18 @@ __global__ __launch_bounds__(BS) AMPH_WIRE_OCC void k_rv_b64(TextSet tx, int n, 
                                            uint32_t pad, uint4* out_y, unsigned long long* ff,
                                            unsigned long long* bad, Fp f) {
   __shared__ uint32_t lds[WireGroups<NP>::bufs < 2 ? 2 : WireGroups<NP>::bufs][3 * BS];
+  __shared__ uint32_t lutw[kLutBytes / 4];
+  uint8_t* lutp = reinterpret_cast<uint8_t*>(lutw);
+  b64_lut_fill(lutp);
+  __syncthreads();
   W4 acc[5];
   uint4 raw[5][NP > 0 ? NP : 1];
   const bool fast = ((size_t)blockIdx.x + 1) * Wire<BS>::chars + 4 <= nchars;
   if (fast) {
     wire_load<NP, BS>(tx, raw, blockIdx.x);
-    wire_fields<NP, BIG, true, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x);
+    wire_fields<NP, BIG, true, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x, lutp);
   } else {
-    wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x);
+    wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x, lutp);
   }
   const size_t word = (size_t)blockIdx.x * Wire<BS>::words + threadIdx.x;
   if (threadIdx.x < Wire<BS>::words) {  // whole waves
@@ -266,6 +273,10 @@ __global__ __launch_bounds__(BS) AMPH_WIRE_OCC void k_mask_b64(TextSet tx, int n
                                              unsigned long long* bad, Fp f) {
   constexpr int WW = Wire<BS>::words;
   __shared__ uint32_t lds[WireGroups<NP>::bufs < 2 ? 2 : WireGroups<NP>::bufs][3 * BS];
+  __shared__ uint32_t lutw[kLutBytes / 4];
+  uint8_t* lutp = reinterpret_cast<uint8_t*>(lutw);
+  b64_lut_fill(lutp);
+  __syncthreads();
   W4 acc[5];
   uint4 raw[5][NP > 0 ? NP : 1];
   const size_t word = (size_t)blockIdx.x * WW + threadIdx.x;
@@ -273,9 +284,9 @@ __global__ __launch_bounds__(BS) AMPH_WIRE_OCC void k_mask_b64(TextSet tx, int n
   const bool fast = ((size_t)blockIdx.x + 1) * Wire<BS>::chars + 4 <= nchars;
   if (fast) {
     wire_load<NP, BS>(tx, raw, blockIdx.x);
-    wire_fields<NP, BIG, true, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x);
+    wire_fields<NP, BIG, true, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x, lutp);
   } else {
-    wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x);
+    wire_fields<NP, BIG, false, BS>(tx, n, nchars, pad, words, raw, lds, acc, bad, f, blockIdx.x, lutp);
   }
   // the secret after the decode: loaded up front it held 4 VGPRs through it
   // (98 VGPRs: 4 waves per SIMD instead of 5); the other waves hide its latency
