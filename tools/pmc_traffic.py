@@ -21,9 +21,14 @@ def kernel_short(name):
     return name.split("(")[0].split("<")[0].split("::")[-1].strip()
 
 
-def per_kernel(path, counter):
+def per_kernel(path, counter, grid=None):
+    """Average per launch; grid: only launches of that Grid_Size (the
+    default bench line also launches k_mask / k_rv on the host phase's
+    4 Mi-word batches, which must not enter the device-resident figure)."""
     vals = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
+        if grid is not None and int(r.get("Grid_Size") or -1) != grid:
+            continue
         if r["Counter_Name"] == counter:
             vals[kernel_short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
@@ -37,8 +42,8 @@ def main():
     ap.add_argument("--parties", type=int, required=True)
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "traffic.json"))
     a = ap.parse_args()
-    f = per_kernel(a.fetch_csv, "FETCH_SIZE")
-    w = per_kernel(a.write_csv, "WRITE_SIZE")
+    f = per_kernel(a.fetch_csv, "FETCH_SIZE", a.words)
+    w = per_kernel(a.write_csv, "WRITE_SIZE", a.words)
     algo = {"k_rv": 80 * a.parties + 16, "k_mask": 80 * a.parties + 32}
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
     for k in ("k_mask", "k_rv"):
