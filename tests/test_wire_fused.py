@@ -75,9 +75,9 @@ def test_rv_b64_matches_oracle(ctx, F, mode, n, W):
 
 @pytest.mark.parametrize("mode", ["host", "device"])
 @pytest.mark.parametrize("W", [4000, 4001, 4002])  # padding 0 / 2 / 1 ('' / '==' / '=')
-def test_rv_b64_bad_characters(ctx, F, mode, W):
-    n = 3
-    odos, _ = F.synth_odos(seed=900 + W, n=n, W=W)
+@pytest.mark.parametrize("n", [3, 5])  # 5: the runtime party-count kernels (NP = 0), same LDS-table decode
+def test_rv_b64_bad_characters(ctx, F, mode, W, n):
+    odos, _ = F.synth_odos(seed=900 + W + n, n=n, W=W)
     base = texts_of(odos)
     nchars = len(base[0][0])
     assert nchars == 4 * ((16 * W + 2) // 3)
@@ -125,15 +125,15 @@ def _first_bad(t: bytes, pad: int) -> int:
 
 
 @pytest.mark.parametrize("W", [64, 65, 66])  # padding '==' / '=' / ''
-def test_rv_b64_mutations(ctx, F, W):
+@pytest.mark.parametrize("n", [2, 5])
+def test_rv_b64_mutations(ctx, F, W, n):
     """Random single-character replacements in a random party's random field:
     an invalid character is reported at its (5 party + field) nchars +
     offset; a valid one changes the decoded word (Python's base64 says how),
     and the verdict and secrets equal the C oracle's on those words."""
     import random
-    rng = random.Random(W)
-    n = 2
-    odos, _ = F.synth_odos(seed=1200 + W, n=n, W=W)
+    rng = random.Random(W + n)
+    odos, _ = F.synth_odos(seed=1200 + W + n, n=n, W=W)
     base = texts_of(odos)
     nchars = len(base[0][0])
     pad = (3 - (16 * W) % 3) % 3
