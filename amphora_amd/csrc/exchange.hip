@@ -127,6 +127,18 @@ __device__ __forceinline__ uint32_t ascii4(uint32_t x) {
   return 0x30303030u | q | ((p - 10u * q) << 8);
 }
 
+// 8 bytes (lo, then hi) ORed into the zeroed LDS text at p, any alignment,
+// as three aligned ds_or_b32: a misaligned 8-byte LDS store costs ~8x an
+// aligned dword op (tools/ubench/ubench_lds_align.hip).
+__device__ __forceinline__ void or_bytes8(char* p, uint32_t lo, uint32_t hi) {
+  const uint32_t mis = (uint32_t)(uintptr_t)p & 3u, sh = 8u * mis;
+  uint32_t* d = reinterpret_cast<uint32_t*>(p - mis);  // (pointer arithmetic: stays an LDS pointer)
+  const uint64_t x = (uint64_t)lo << sh, y = (uint64_t)hi << sh;
+  atomicOr(d, (uint32_t)x);
+  atomicOr(d + 1, (uint32_t)(x >> 32) | (uint32_t)y);
+  atomicOr(d + 2, (uint32_t)(y >> 32));
+}
+
 // nd decimal digits of the chunks ch (to_chunks) at o; returns o + nd.
 __device__ __forceinline__ char* put_digits(char* o, const uint32_t (&ch)[5], int nd) {
   // chunk k (base 10^9, little end first) holds text positions
@@ -139,10 +151,9 @@ __device__ __forceinline__ char* put_digits(char* o, const uint32_t (&ch)[5], in
     const uint32_t c = ch[k], top = c / 100000000u, r = c - top * 100000000u;
     const uint32_t hi = r / 10000u;
     const uint32_t w0 = ascii4(hi), w1 = ascii4(r - hi * 10000u);
-    if (base >= 0) {  // a whole chunk: 1 byte + two (unaligned) 4-byte LDS stores
+    if (base >= 0) {  // a whole chunk: 1 byte + 8 ORed into the zeroed run
       o[base] = (char)(0x30u + top);
-      __builtin_memcpy(o + base + 1, &w0, 4);
-      __builtin_memcpy(o + base + 5, &w1, 4);
+      or_bytes8(o + base + 1, w0, w1);
       continue;
     }
     const uint32_t dig[9] = {0x30u + top,      w0 & 0xFFu,         (w0 >> 8) & 0xFFu,
@@ -344,6 +355,8 @@ __global__ __launch_bounds__(kXBlock) void k_xenc_write(const uint4* mag, const 
   int nd = 0, ne = 0;
   bool sd = false, se = false;
   uint32_t len = 0, total;  // <= 92 per entry, <= 23 552 per workgroup
+  // the run's digits are ORed in (or_bytes8): zero the buffer (block_excl_scan32's barriers order it)
+  for (int q = threadIdx.x; q < (int)(sizeof(bufv) / 16); q += kXBlock) bufv[q] = make_uint4(0, 0, 0, 0);
   if (k < npairs) {
     const uint4 d = mag[2 * k], e = mag[2 * k + 1];
     const uint32_t ng = reinterpret_cast<const uint16_t*>(neg)[k];  // (loaded beside the magnitudes)
