@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-5 closing evidence: smoke, then tools/gpu_prof.sh (the default bench
-# line, rocprofv3 --kernel-trace --stats of the same command, FETCH_SIZE and
+# line, rocprofv3 --kernel-trace --stats of the same command (full template
+# names: the host phase's 3-party batch launches are listed apart), FETCH_SIZE and
 # WRITE_SIZE passes).
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
