@@ -143,6 +143,33 @@ int main(int argc, char** argv) {
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       if (r >= 3) tsp.push_back(ms);
     }
+#ifdef XDEC_STAMPS
+    {  // one more span decode with per-block phase clocks (thread 0 of each workgroup)
+      unsigned long long* st;
+      CK(hipMalloc(&st, 8 * 8 * x.nb));
+      CK(hipMemset(st, 0, 8 * 8 * x.nb));
+      CK(hipMemcpyToSymbol(HIP_SYMBOL(g_xstamps), &st, sizeof(st)));
+      CK(hipMemset(bad, 0x7F, 8));
+      CK(launch_exchange_decode_spans(text, L, npairs, x, bad, s3, c));
+      CK(hipDeviceSynchronize());
+      unsigned long long* none = nullptr;
+      CK(hipMemcpyToSymbol(HIP_SYMBOL(g_xstamps), &none, sizeof(none)));
+      std::vector<unsigned long long> h(8 * x.nb);
+      CK(hipMemcpy(h.data(), st, 8 * 8 * x.nb, hipMemcpyDeviceToHost));
+      double sum[6] = {0};
+      size_t cntb = 0;
+      for (size_t b = 1; b + 1 < x.nb; ++b) {
+        const unsigned long long* t = &h[8 * b];
+        if (!t[0] || !t[5]) continue;
+        for (int i = 1; i <= 5; ++i) sum[i] += (double)(t[i] - t[i - 1]);
+        ++cntb;
+      }
+      printf("stamps (clock64 cycles per workgroup, mean over %zu): staging %.0f, colons+scan %.0f, pos+barrier %.0f, "
+             "parse (wave 0) %.0f, final barrier %.0f, total %.0f\n", cntb, sum[1] / cntb, sum[2] / cntb, sum[3] / cntb,
+             sum[4] / cntb, sum[5] / cntb, (sum[1] + sum[2] + sum[3] + sum[4] + sum[5]) / cntb);
+      CK(hipFree(st));
+    }
+#endif
     CK(hipMemset(mag2, 0, nvals * 16)); CK(hipMemset(neg2, 0, nvals));
     hipLaunchKernelGGL(k_unspan, dim3((unsigned)((npairs + 127) / 128)), dim3(128), 0, 0, x, npairs, mag2, neg2);
     CK(hipDeviceSynchronize());
