@@ -567,6 +567,34 @@ def test_exchange_decode_block_boundaries(ctx):
         assert np.array_equal(n2, neg_exp)
 
 
+def test_exchange_decode_every_length_and_the_2_128_edge(ctx):
+    """The compact pass's number boundaries: every digit count 1..39 at its
+    smallest and largest value (the largest 39-digit one is 2^128 - 1), both
+    signs, at shifted offsets (the 8-digit chunk and span boundaries move);
+    then 2^128 and a 40-digit value must be rejected where a compact text
+    holds them (Jackson reads BigInteger, the field word is 128 bits)."""
+    vals = []
+    for L in range(1, 40):
+        lo, hi = 10 ** (L - 1) if L > 1 else 0, min(10 ** L - 1, 2 ** 128 - 1)
+        vals += [lo, -hi, hi, -lo if lo else 0]
+    pairs = [(vals[2 * k], vals[2 * k + 1]) for k in range(len(vals) // 2)] * 40  # ~3 k pairs, several spans
+    text = json.dumps([{"a": a, "b": b} for a, b in pairs], separators=(",", ":")).encode()
+    mag, neg = _diff_arrays(pairs)
+    assert ctx.exchange_encode(mag, neg) == text  # the formatter at every length too
+    for off in (0, 3, 7):
+        m2, n2 = ctx.exchange_decode(b" " * off + text, len(pairs))
+        assert np.array_equal(m2, mag)
+        neg_exp = neg.copy()
+        neg_exp[(mag == 0).all(axis=2)] = 0
+        assert np.array_equal(n2, neg_exp)
+    for bad in (2 ** 128, -(2 ** 128), 10 ** 39, 2 ** 129):
+        p2 = list(pairs)
+        p2[len(p2) // 2] = (bad, 1)
+        t2 = json.dumps([{"a": a, "b": b} for a, b in p2], separators=(",", ":")).encode()
+        with pytest.raises(ValueError, match="offset"):
+            ctx.exchange_decode(t2, len(p2))
+
+
 def test_exchange_decode_count_and_brackets(ctx):
     with pytest.raises(ValueError, match="exactly 3 FactorPairs"):
         ctx.exchange_decode(b'[{"a":1,"b":2},{"a":3,"b":4}]', 3)
