@@ -24,7 +24,7 @@
 // validated without a second pass; the first malformed byte's offset is
 // reported.  Whitespace between tokens is accepted, as in any JSON reader.
 //
-// Decimal conversion: 128-bit magnitude <-> five base-10^9 chunks (a
+// Decimal conversion: 128-bit magnitude <-> five base-10^8 chunks (a
 // multiply-accumulate over the limbs with four carry divisions by a constant,
 // to_chunks), chunks <-> digits.
 #include <hip/hip_ext.h>
@@ -57,59 +57,47 @@ constexpr int kXBlock = 256;      // pairs per workgroup (encode)
 constexpr int kXEntry = 92;       // max entry: {"a":-<39 digits>,"b":-<39 digits>},
 constexpr int kScanBlock = 1024;  // elements per workgroup of the scan passes
 constexpr int kDecBytes = 32;     // text bytes per lane (decode)
-constexpr uint64_t kE9 = 1000000000ull;
 
-__device__ __forceinline__ int ndigits32(uint32_t x) {  // x < 10^9; 0 -> 1
+__device__ __forceinline__ int ndigits32(uint32_t x) {  // x < 10^9; 0 -> 1 (to_chunks' top chunk: < 10^8)
   int n = 1;
 #pragma unroll
   for (uint32_t t = 10; t <= 100000000u; t *= 10) n += x >= t;
   return n;
 }
 
-// One base-2^32 long-division step by 10^9: (rem, x) -> quotient, rem updated.
-__device__ __forceinline__ uint32_t div_step_e9(uint64_t& rem, uint32_t x) {
-  const uint64_t cur = (rem << 32) | x;
-  const uint64_t q = cur / kE9;  // < 2^32: rem < 10^9
-  rem = cur - q * kE9;
-  return (uint32_t)q;
-}
-
-// 128-bit magnitude -> base-10^9 chunks (little end first); returns the
-// decimal digit count (1 for zero).  Multiply-accumulate form: with the limbs
-// x_i of x = sum x_i 2^(32 i) and the base-10^9 digits of 2^32, 2^64, 2^96
-//   2^32 = 4 | 294967296,  2^64 = 18 | 446744073 | 709551616,
-//   2^96 = 79 | 228162514 | 264337593 | 543950336,
-// column k of the base-10^9 product sum is A_k = carry + sum x_i c_(i,k):
-// nine v_mad_u64_u32 and one carry division per column (ten 64-by-32-bit
-// division steps by a constant became four: 12 % fewer VALU in k_xenc_write).
-// Bounds (x_i < 2^32): A_0 < 6.7e18 (its high word can reach 1.55e9, so one
-// 32-bit division takes it below 10^9 first), A_1 < 3.1e18, A_2 < 1e18,
-// A_3 < 3.5e11 -- each high word < 10^9, as div_step_e9 requires, and every
-// quotient < 2^32 except A_0's (< 2^33, kept as qa:q0).
 __device__ __forceinline__ uint64_t mad_u64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
 
+// 128-bit magnitude -> base-10^8 chunks (little end first); returns the
+// decimal digit count (1 for zero).  Multiply-accumulate form: with the limbs
+// x_i of x = sum x_i 2^(32 i) and the base-10^8 digits of 2^32, 2^64, 2^96
+//   2^32 = 42 | 94967296,  2^64 = 1844 | 67440737 | 09551616,
+//   2^96 = 79228 | 16251426 | 43375935 | 43950336,
+// column k of the base-10^8 product sum is D_k = carry + sum x_i c_(i,k):
+// nine v_mad_u64_u32 and four carry divisions by 10^8 in all.  Bounds
+// (x_i < 2^32): D_0 < 6.4e17, D_1 < 4.8e17, D_2 < 7.0e16, D_3 < 3.5e14, each
+// < 2^64; the last carry (< 3.5e6) is chunk 4 (x < 2^128: <= 7 digits).
+// Base 10^8 rather than 10^9: a chunk is exactly two 4-digit halves, so the
+// formatter has no separate leading digit per chunk (k_xenc_write -1.5 %,
+// profiles/r05_xenc_base1e8_ab.txt; the base-10^9 form: r05_xenc_mac_ab.txt).
 __device__ __forceinline__ int to_chunks(const uint4& m, uint32_t (&ch)[5]) {
-  uint64_t A = mad_u64(m.w, 543950336u, mad_u64(m.z, 709551616u, mad_u64(m.y, 294967296u, m.x)));
-  const uint32_t ah = (uint32_t)(A >> 32), qa = ah / (uint32_t)kE9;  // qa <= 1
-  uint64_t rem = ah - qa * (uint32_t)kE9;
-  const uint64_t q0 = ((uint64_t)qa << 32) | div_step_e9(rem, (uint32_t)A);
-  ch[0] = (uint32_t)rem;
-  A = mad_u64(m.w, 264337593u, mad_u64(m.z, 446744073u, mad_u64(m.y, 4u, q0)));
-  rem = A >> 32;
-  const uint32_t q1 = div_step_e9(rem, (uint32_t)A);
-  ch[1] = (uint32_t)rem;
-  A = mad_u64(m.w, 228162514u, mad_u64(m.z, 18u, q1));
-  rem = A >> 32;
-  const uint32_t q2 = div_step_e9(rem, (uint32_t)A);
-  ch[2] = (uint32_t)rem;
-  A = mad_u64(m.w, 79u, q2);
-  rem = A >> 32;
-  ch[4] = div_step_e9(rem, (uint32_t)A);  // x / 10^36 < 2^8.4
-  ch[3] = (uint32_t)rem;
+  constexpr uint64_t kE8 = 100000000ull;
+  uint64_t D = mad_u64(m.w, 43950336u, mad_u64(m.z, 9551616u, mad_u64(m.y, 94967296u, m.x)));
+  uint64_t q = D / kE8;
+  ch[0] = (uint32_t)(D - q * kE8);
+  D = mad_u64(m.w, 43375935u, mad_u64(m.z, 67440737u, mad_u64(m.y, 42u, q)));
+  q = D / kE8;
+  ch[1] = (uint32_t)(D - q * kE8);
+  D = mad_u64(m.w, 16251426u, mad_u64(m.z, 1844u, q));
+  q = D / kE8;
+  ch[2] = (uint32_t)(D - q * kE8);
+  D = mad_u64(m.w, 79228u, q);
+  q = D / kE8;
+  ch[3] = (uint32_t)(D - q * kE8);
+  ch[4] = (uint32_t)q;
   int top = 0;
 #pragma unroll
   for (int k = 1; k < 5; ++k) top = ch[k] ? k : top;
-  return 9 * top + ndigits32(ch[top]);
+  return 8 * top + ndigits32(ch[top]);
 }
 
 __device__ __forceinline__ char* put_str(char* o, const char* s) {
@@ -139,28 +127,24 @@ __device__ __forceinline__ void or_bytes8(char* p, uint32_t lo, uint32_t hi) {
   atomicOr(d + 2, (uint32_t)(y >> 32));
 }
 
-// nd decimal digits of the chunks ch (to_chunks) at o; returns o + nd.
+// nd decimal digits of the chunks ch (to_chunks, base 10^8) at o; returns o + nd.
 __device__ __forceinline__ char* put_digits(char* o, const uint32_t (&ch)[5], int nd) {
-  // chunk k (base 10^9, little end first) holds text positions
-  // [nd - 9 (k + 1), nd - 9 k); its 9 digits come from one division by 10^8,
-  // one by 10^4 and two 4-digit SWAR conversions instead of 9 divisions by 10
+  // chunk k (little end first) holds text positions [nd - 8 (k + 1), nd - 8 k):
+  // one division by 10^4 and two 4-digit SWAR conversions
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
-    const int base = nd - 9 * (k + 1);
-    if (base + 9 <= 0) break;
-    const uint32_t c = ch[k], top = c / 100000000u, r = c - top * 100000000u;
-    const uint32_t hi = r / 10000u;
-    const uint32_t w0 = ascii4(hi), w1 = ascii4(r - hi * 10000u);
-    if (base >= 0) {  // a whole chunk: 1 byte + 8 ORed into the zeroed run
-      o[base] = (char)(0x30u + top);
-      or_bytes8(o + base + 1, w0, w1);
+    const int base = nd - 8 * (k + 1);
+    if (base + 8 <= 0) break;
+    const uint32_t c = ch[k], hi = c / 10000u;
+    const uint32_t w0 = ascii4(hi), w1 = ascii4(c - hi * 10000u);
+    if (base >= 0) {  // a whole chunk: 8 bytes ORed into the zeroed run
+      or_bytes8(o + base, w0, w1);
       continue;
     }
-    const uint32_t dig[9] = {0x30u + top,      w0 & 0xFFu,         (w0 >> 8) & 0xFFu,
-                             (w0 >> 16) & 0xFFu, w0 >> 24,          w1 & 0xFFu,
-                             (w1 >> 8) & 0xFFu,  (w1 >> 16) & 0xFFu, w1 >> 24};
+    const uint32_t dig[8] = {w0 & 0xFFu, (w0 >> 8) & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
+                             w1 & 0xFFu, (w1 >> 8) & 0xFFu, (w1 >> 16) & 0xFFu, w1 >> 24};
 #pragma unroll
-    for (int j = 0; j < 9; ++j)
+    for (int j = 0; j < 8; ++j)
       if (base + j >= 0) o[base + j] = (char)dig[j];
   }
   return o + nd;
@@ -313,7 +297,7 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_apply(uint64_t* x, size_t n
 
 // Encode pass 1: the text length of each workgroup's run of entries
 // (bs[g] = sum of the entry lengths of pairs [256 g, 256 g + 256)); digit
-// counts from the bit length (ndigits128), not the base-10^9 split.
+// counts from the bit length (ndigits128), not the base-10^8 split.
 __global__ __launch_bounds__(4 * kXBlock) void k_xenc_bsum(const uint4* mag, const uint8_t* neg,
                                                        size_t npairs, size_t nb, uint64_t* bs) {
   // one pair per lane, 4 sub-blocks of 256 pairs per 1024-lane workgroup:
