@@ -301,15 +301,35 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_apply(uint64_t* x, size_t n
 __global__ __launch_bounds__(4 * kXBlock) void k_xenc_bsum(const uint4* mag, const uint8_t* neg,
                                                        size_t npairs, size_t nb, uint64_t* bs) {
   // one pair per lane, 4 sub-blocks of 256 pairs per 1024-lane workgroup:
-  // wave sums by shuffles, then 4 lanes add their sub-block's 4 wave sums
+  // wave sums by shuffles, then 4 lanes add their sub-block's 4 wave sums.
+  // The powers of ten ndigits128 compares with sit in LDS (a global table
+  // made its lookup a second dependent memory round trip per number).
   __shared__ uint32_t ws[16];
+  __shared__ uint4 p10[39];
+  if (threadIdx.x < 39)
+    p10[threadIdx.x] = make_uint4(kPow10[threadIdx.x][0], kPow10[threadIdx.x][1], kPow10[threadIdx.x][2],
+                                  kPow10[threadIdx.x][3]);
   const size_t k = (size_t)blockIdx.x * (4 * kXBlock) + threadIdx.x;
+  uint4 d = make_uint4(0, 0, 0, 0), e = d;
+  uint32_t ng = 0;
+  if (k < npairs) {
+    d = mag[2 * k];
+    e = mag[2 * k + 1];
+    ng = reinterpret_cast<const uint16_t*>(neg)[k];
+  }
+  __syncthreads();
   uint32_t len = 0;
-  if (k < npairs)
-  {  // {"a":A,"b":B} (+ ',' unless last)
-    const uint4 d = mag[2 * k], e = mag[2 * k + 1];
-    len = 11 + ndigits128(d) + (neg[2 * k] != 0 && !is_zero(d)) + ndigits128(e) +
-          (neg[2 * k + 1] != 0 && !is_zero(e)) + (k + 1 < npairs);
+  if (k < npairs) {  // {"a":A,"b":B} (+ ',' unless last)
+    auto nd = [&](const uint4& m) {
+      const int bits = m.w ? 128 - __clz(m.w) : m.z ? 96 - __clz(m.z) : m.y ? 64 - __clz(m.y) : 32 - __clz(m.x);
+      const int t = (bits * 1233) >> 12;
+      const uint4 p = p10[t];
+      const uint32_t pa[4] = {p.x, p.y, p.z, p.w};
+      const int n = t + (ge128(m, pa) ? 1 : 0);
+      return n ? n : 1;
+    };
+    len = 11 + nd(d) + ((ng & 0xFFu) != 0 && !is_zero(d)) + nd(e) + ((ng >> 8) != 0 && !is_zero(e)) +
+          (k + 1 < npairs);
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) len += __shfl_xor(len, o, 64);
