@@ -105,3 +105,31 @@ def test_codec_edges(ctx, F, vals):
     assert [int.from_bytes(x.tobytes(), "little") for x in ctx.from_gfp(a)] == \
         [spdz.from_gfp(x.tobytes()) for x in a]
     assert [x.tobytes() for x in ctx.to_gfp(a)] == [spdz.to_gfp(v % P) for v in vals]
+
+
+# signed diffs as the Beaver exchange carries them: magnitudes < 2^128 with
+# every decimal length and the 10^k / 2^k edges
+_DEC_EDGE = sorted({v for k in range(39) for v in (10 ** k - 1, 10 ** k, 10 ** k + 1) if 0 <= v < 2 ** 128} |
+                   {v for k in range(129) for v in (2 ** k - 1, 2 ** k) if v < 2 ** 128})
+signed_diff = st.builds(lambda m, s: -m if s else m,
+                        st.one_of(st.sampled_from(_DEC_EDGE), st.integers(0, 2 ** 128 - 1),
+                                  st.integers(0, 10 ** 12)), st.booleans())
+
+
+@SETTINGS
+@given(st.lists(st.tuples(signed_diff, signed_diff), min_size=1, max_size=300))
+def test_exchange_codec_edges(ctx, pairs):
+    """MultiplicationExchangeObject interimValues: the GPU encode is byte-for-byte
+    Jackson's compact text (json.dumps with BigInteger semantics: no "-0"), and
+    the GPU decode of that text gives back the signed values."""
+    import json
+    text = json.dumps([{"a": a, "b": b} for a, b in pairs], separators=(",", ":")).encode()
+    mag = np.zeros((len(pairs), 2, 16), np.uint8)
+    neg = np.zeros((len(pairs), 2), np.uint8)
+    for k, ab in enumerate(pairs):
+        for j, x in enumerate(ab):
+            mag[k, j] = np.frombuffer(abs(x).to_bytes(16, "little"), np.uint8)
+            neg[k, j] = x < 0
+    assert ctx.exchange_encode(mag, neg) == text
+    m2, n2 = ctx.exchange_decode(text, len(pairs))
+    assert np.array_equal(m2, mag) and np.array_equal(n2, neg)
