@@ -757,8 +757,13 @@ __device__ __forceinline__ bool fast_segment(const uint32_t* l32, uint32_t o, ui
                                              size_t nvals, size_t xo, size_t len, FastNum& r) {
   const uint32_t pre = lds_dword(l32, o - 4);
   r.key = (pre >> 8) & 0xFFu;
-  bool ok = (pre & 0xFFFF00FFu) == 0x3A220022u && (r.key == 'a' || r.key == 'b');
-  if (g == 0) ok = ok && xo == 6 && (lds_dword(l32, o - 6) & 0xFFFFu) == 0x7B5Bu;  // "[{"
+  // '"' k '"' ':' before a value was already checked as the end of the
+  // previous value's segment (its after_ok); only the text's first value
+  // has no previous one
+  bool ok = true;
+  if (g == 0)
+    ok = (pre & 0xFFFF00FFu) == 0x3A220022u && (r.key == 'a' || r.key == 'b') && xo == 6 &&
+         (lds_dword(l32, o - 6) & 0xFFFFu) == 0x7B5Bu;  // "[{"
   const uint32_t key = r.key;
   return fast_parse(l32, o, ok, r, [=](uint32_t dend) {
     const uint32_t a0 = lds_dword(l32, dend), a1 = lds_dword(l32, dend + 4);
@@ -792,10 +797,16 @@ __device__ __forceinline__ uint32_t fast_value(const uint32_t* l32, uint32_t o, 
   r.key = (pre >> 16) & 0xFFu;
   const uint32_t lead = pre & 0xFFu;
   const bool m1 = lead == (uint32_t)',';
-  bool ok = (pre & 0xFF00FF00u) == 0x22002200u && (r.key == 'a' || r.key == 'b') &&
-            (lead == (uint32_t)'{' || m1) && (lds_dword(l32, o - 1) & 0xFFu) == (uint32_t)':';
+  // the bytes before the value were checked as the end of the previous
+  // value's segment (its after_ok), except for the text's first value: it
+  // must be SEG_FIRST, and only it gets the full check here
+  bool ok = true;
   uint32_t flags = m1 ? SEG_M1 : 0;
-  if (xo == 6 && (lds_dword(l32, o - 6) & 0xFFFFu) == 0x7B5Bu) flags |= SEG_FIRST;  // "[{"
+  if (xo == 6) {
+    ok = (pre & 0xFF00FF00u) == 0x22002200u && (r.key == 'a' || r.key == 'b') && lead == (uint32_t)'{' &&
+         (lds_dword(l32, o - 1) & 0xFFu) == (uint32_t)':';
+    if ((lds_dword(l32, o - 6) & 0xFFFFu) == 0x7B5Bu) flags |= SEG_FIRST;  // "[{"
+  }
   const uint32_t key = r.key;
   ok = fast_parse(l32, o, ok, r, [&](uint32_t dend) {
     const uint32_t a0 = lds_dword(l32, dend), a1 = lds_dword(l32, dend + 4);
