@@ -586,19 +586,19 @@ __device__ __forceinline__ uint32_t pow10_small(uint32_t k) {  // k <= 7
   return __umul24(__umul24((k & 1u) ? 10u : 1u, (k & 2u) ? 100u : 1u), (k & 4u) ? 10000u : 1u);
 }
 
-// Length of the digit run at the start of the 44 bytes d[0..10] (44 if all
-// are digits): SWAR non-digit flags (0x80 per byte), packed one bit per byte
-// by v_dot4_u32_u8 as in colons32, and one 64-bit count of trailing zeros
-// (where a compare-and-select chain over the 11 dwords took twice the VALU).
-__device__ __forceinline__ uint32_t digit_run(const uint32_t (&d)[11]) {
-  uint64_t mask = 1ull << 44;
+// Length of the digit run at the start of the 40 bytes d[0..9], capped at
+// 40 (a number has at most 39 digits, so a run reaching byte 40 is already a
+// rejection): SWAR non-digit flags (0x80 per byte), packed one bit per byte by
+// v_dot4_u32_u8 as in colons32, and one 64-bit count of trailing zeros (where
+// a compare-and-select chain over the dwords took twice the VALU).
+__device__ __forceinline__ uint32_t digit_run(const uint32_t (&d)[10]) {
+  uint64_t mask = 1ull << 40;
 #pragma unroll
-  for (int q = 0; q < 6; ++q) {
+  for (int q = 0; q < 5; ++q) {
     uint32_t nd2[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int j = 2 * q + h;
-      const uint32_t x = (j < 11 ? d[j] : 0u) ^ 0x30303030u;  // digits -> 0..9
+      const uint32_t x = d[2 * q + h] ^ 0x30303030u;  // digits -> 0..9
       nd2[h] = (((x & 0x7F7F7F7Fu) + 0x76767676u) | x) & 0x80808080u;
     }
     const uint32_t a = __builtin_amdgcn_udot4(nd2[0], 0x08040201u,
@@ -613,7 +613,7 @@ __device__ __forceinline__ uint32_t digit_run(const uint32_t (&d)[11]) {
 //   member 1:                <digit> ',' '"' k '"' ':' NUM '}'
 // with every byte read from the LDS window as whole dwords (independent
 // ds_read_b32 + v_alignbyte, no byte-by-byte walk): the digit run is found
-// with SWAR over 44 bytes held in registers, and the value is folded in
+// with SWAR over 40 bytes held in registers, and the value is folded in
 // base 10^8 from the same registers: full 8-digit chunks, then the partial
 // last chunk right-aligned behind '0's.  Returns false for anything else
 // (whitespace, the first or last pair, a leading zero, more than 39 digits,
@@ -635,7 +635,7 @@ __device__ __forceinline__ uint32_t lds_dword(const uint32_t* l32, uint32_t o) {
 // The number at window offset o: '-'? then 1..39 digits without a leading
 // zero, value < 2^128, followed by what after_ok(one past its last digit)
 // accepts (sets r.v, r.minus, r.dend; ok: the caller's own checks so far).
-// The digit run is found with SWAR over 44 bytes held in registers; the
+// The digit run is found with SWAR over 40 bytes held in registers; the
 // value is folded in base 10^8 from the same registers: full 8-digit
 // chunks, then the nd % 8 leading digits of the next chunk right-aligned
 // behind '0's.
@@ -645,9 +645,9 @@ __device__ __forceinline__ bool fast_parse(const uint32_t* l32, uint32_t o, bool
   const uint32_t first = lds_dword(l32, o);
   r.minus = (first & 0xFFu) == (uint32_t)'-';
   const uint32_t ds = o + (r.minus ? 1u : 0u);
-  uint32_t d[11];
+  uint32_t d[10];
 #pragma unroll
-  for (int j = 0; j < 11; ++j) d[j] = lds_dword(l32, ds + 4 * j);
+  for (int j = 0; j < 10; ++j) d[j] = lds_dword(l32, ds + 4 * j);
   const uint32_t nd = digit_run(d);
   ok = ok && nd >= 1 && nd <= 39 && !((d[0] & 0xFFu) == (uint32_t)'0' && nd > 1);
   if (!ok) return false;
@@ -703,9 +703,9 @@ __device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, boo
   const uint32_t first = lds_dword(l32, o);
   r.minus = (first & 0xFFu) == (uint32_t)'-';
   const uint32_t ds = o + (r.minus ? 1u : 0u);
-  uint32_t d[11];
+  uint32_t d[10];
 #pragma unroll
-  for (int j = 0; j < 11; ++j) d[j] = lds_dword(l32, ds + 4 * j);
+  for (int j = 0; j < 10; ++j) d[j] = lds_dword(l32, ds + 4 * j);
   const uint32_t nd = digit_run(d);
   ok = ok && nd >= 1 && nd <= 39 && !((d[0] & 0xFFu) == (uint32_t)'0' && nd > 1);
   if (!ok) return false;
