@@ -481,17 +481,30 @@ constexpr int kWin = (int)kDecSpan + 2 * kWinPad;      // staged bytes
 // 256-lane workgroup.  96 us per 640 MB text where 128 lanes x 64
 // lane-contiguous bytes per span took 162 (tools/ubench/ubench_xcount.hip).
 constexpr int kCntWaves = 4;
+// Numbers (colons) per 8 KiB span at most: {"a":1,"b":2}, is 14 bytes per 2
+constexpr int kMaxStarts = 1280;
+constexpr int kListHead = 256;  // colon-list entries per span in the list's dense head
+
+// A 16-byte chunk's colons, one bit per byte (as colons32)
+__device__ __forceinline__ uint32_t colons16(const uint4& c) {
+  const uint32_t h0 = __builtin_amdgcn_udot4(swar_colon(c.y), 0x80402010u, 0u, false);
+  const uint32_t a0 = __builtin_amdgcn_udot4(swar_colon(c.x), 0x08040201u, h0, false);
+  const uint32_t h1 = __builtin_amdgcn_udot4(swar_colon(c.w), 0x80402010u, 0u, false);
+  const uint32_t a1 = __builtin_amdgcn_udot4(swar_colon(c.z), 0x08040201u, h1, false);
+  return (a0 >> 7) | ((a1 >> 7) << 8);
+}
 
 __device__ __forceinline__ uint32_t swar_below21(uint32_t w) {  // nonzero iff some byte < 0x21
   return (w - 0x21212121u) & ~w & 0x80808080u;
 }
 
 __global__ __launch_bounds__(64 * kCntWaves) void k_xdec_count(Text t, uint64_t* bsum, size_t nb,
-                                                             unsigned int* slow) {
+                                                             unsigned int* slow, uint16_t* posg) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *slow = 0;  // k_xdec_fast's flag
   const size_t span = (size_t)blockIdx.x * kCntWaves + (threadIdx.x >> 6);
   if (span >= nb) return;
-  const size_t base = span * kDecSpan + (size_t)(threadIdx.x & 63) * 16;
+  const uint32_t lane = threadIdx.x & 63;
+  const size_t base = span * kDecSpan + (size_t)lane * 16;
   uint4 c[8];
   if (span * kDecSpan >= t.mis && (span + 1) * kDecSpan <= t.L) {
 #pragma unroll
@@ -503,19 +516,55 @@ __global__ __launch_bounds__(64 * kCntWaves) void k_xdec_count(Text t, uint64_t*
 #pragma unroll
     for (int k = 0; k < 8; ++k) c[k] = t.chunk((long long)(base + 1024 * k));
   }
-  uint32_t cnt = 0, low = 0;
+  uint32_t msk[8], low = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    cnt += __popc(swar_colon(c[k].x)) + __popc(swar_colon(c[k].y)) + __popc(swar_colon(c[k].z)) +
-           __popc(swar_colon(c[k].w));
+    msk[k] = colons16(c[k]);
     low |= swar_below21(c[k].x) | swar_below21(c[k].y) | swar_below21(c[k].z) | swar_below21(c[k].w);
   }
+  // The span's colon list (k_xdec_fast's values, in text order: slab k =
+  // bytes 1024k.., lane by lane): per-slab lane prefixes by DPP scans of two
+  // slabs' counts per word (<= 1024 each), slab bases by running the totals;
+  // listed in LDS, then stored as 16-byte chunks.  At 8 Mi pairs the list
+  // (~34 MB) costs this pass ~16 us and saves k_xdec_fast ~34 (its colon
+  // scan, workgroup scan and barrier), r05_xdec_colon_list_ab.txt.
+  __shared__ uint4 lp4[kCntWaves][kMaxStarts / 8 + 8];  // (+ one dummy slot per lane)
+  uint16_t* lp = reinterpret_cast<uint16_t*>(lp4[threadIdx.x >> 6]);
+  uint32_t cnt = 0;
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t pk = __popc(msk[2 * q]) | (__popc(msk[2 * q + 1]) << 16);
+    const uint32_t inc = wave_incl_scan32(pk);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63), ex = inc - pk;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint32_t i = cnt + ((ex >> (16 * h)) & 0xFFFFu);
+      cnt += (tot >> (16 * h)) & 0xFFFFu;
+      // the lane's first colon without a branch (none: a dummy slot of its
+      // own), the rare rest in a loop taken only when some lane has more
+      uint32_t m = msk[2 * q + h];
+      const uint32_t at0 = 1024 * (2 * q + h) + 16 * lane - 1;
+      lp[m && i < (uint32_t)kMaxStarts ? i : kMaxStarts + lane] = (uint16_t)(at0 + __ffs(m));
+      m &= m - 1;
+      if (__ballot(m != 0) != 0)
+        for (++i; m && i < (uint32_t)kMaxStarts; m &= m - 1, ++i) lp[i] = (uint16_t)(at0 + __ffs(m));
+    }
+  }
+  if (posg) {  // (this wave's own LDS writes: in order, no workgroup barrier)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the first kListHead entries of every span side by side (the spans of a
+    // workgroup write one stretch), the rest (short numbers only) after them
+    uint4* head = reinterpret_cast<uint4*>(posg + span * kListHead);
+    uint4* tail = reinterpret_cast<uint4*>(posg + nb * kListHead + span * (kMaxStarts - kListHead)) - kListHead / 8;
+    const uint32_t n16 = (min(cnt, (uint32_t)kMaxStarts) + 7) / 8;
+    for (uint32_t u = lane; u < n16; u += 64) (u < kListHead / 8 ? head : tail)[u] = lp4[threadIdx.x >> 6][u];
+  }
   // whitespace (or a control byte) in a span wholly inside the text: the
   // compact fast pass cannot hold, so it is skipped (kWsBit, summed by the scan)
   const bool ws = span * kDecSpan >= t.mis && (span + 1) * kDecSpan <= t.L && __ballot(low != 0) != 0;
-  if ((threadIdx.x & 63) == 0) bsum[span] = cnt | (ws ? kWsBit : 0);
+  if (lane == 0) bsum[span] = cnt | (ws ? kWsBit : 0);
 }
 
 // The workgroup's 8 KiB span plus kWinPad bytes either side, staged in LDS;
@@ -862,8 +911,7 @@ __device__ __forceinline__ void array_check(const Text& t, uint64_t total, size_
 // ties each member 1 to the member 0 before it (same ',', other key), so
 // together they cover every byte of a well-formed array.  A well-formed text
 // has at most kMaxStarts numbers per 8 KiB span ({"a":1,"b":2}, = 14 bytes per 2);
-// a colon beyond that is reported as malformed.
-constexpr int kMaxStarts = 1280;
+// a colon beyond that is reported as malformed (kMaxStarts, above).
 
 // Launched on at most kSlowGrid workgroups, each taking spans blockIdx.x,
 // + gridDim.x, ...: when the compact pass held, every workgroup returns at
@@ -1096,10 +1144,14 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_slow(Text text, Bases bs, si
 // takes it.
 __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64_t* bscan, size_t nb,
                                                      size_t nvals, uint4* mag, uint8_t* neg,
-                                                     unsigned int* slow) {
+                                                     unsigned int* slow, const uint16_t* posg) {
   if ((bscan[nb] & ~kCountMask) != 0) return;  // whitespace somewhere: the general pass does it all
   __shared__ uint4 win4[kWin / 16 + 1];
-  __shared__ uint16_t pos[kMaxStarts];  // colon, relative to b0
+  // the count pass's colon list (relative to b0); the first 256 read with the
+  // window (entries past the span's count are unused)
+  static_assert(kListHead == kDecBlock, "one head entry per lane");
+  const uint32_t p0 = posg[(size_t)blockIdx.x * kListHead + threadIdx.x];
+  const uint16_t* pl = posg + nb * kListHead + (size_t)blockIdx.x * (kMaxStarts - kListHead) - kListHead;
   const size_t b0 = (size_t)blockIdx.x * kDecSpan;
   const long long w0 = (long long)b0 - kWinPad;
   if (w0 >= (long long)text.mis && w0 + 16LL * (kWin / 16 + 1) <= (long long)text.L) {
@@ -1119,22 +1171,14 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64
     for (int c = threadIdx.x; c < kWin / 16 + 1; c += kDecBlock) win4[c] = text.chunk(w0 + 16LL * c);
   }
   __syncthreads();
-  const int lo = kWinPad + kDecBytes * threadIdx.x;
-  const uint4 c0 = win4[lo / 16], c1 = win4[lo / 16 + 1];
-  const uint32_t w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-  uint32_t m = colons32(w);
-  uint32_t total;
-  const uint32_t first = block_excl_scan32(__popc(m), &total);
-  for (int k = (int)first; m && k < kMaxStarts; m &= m - 1, ++k)
-    pos[k] = (uint16_t)(kDecBytes * threadIdx.x + __ffs(m) - 1);
-  __syncthreads();
+  const uint64_t gbase = bscan[blockIdx.x] & kCountMask;
+  const uint32_t total = (uint32_t)((bscan[blockIdx.x + 1] & kCountMask) - gbase);
   bool fail = total > (uint32_t)kMaxStarts;
   const uint32_t nloc = min(total, (uint32_t)kMaxStarts);
-  const uint64_t gbase = bscan[blockIdx.x] & kCountMask;
   const uint32_t* l32 = reinterpret_cast<const uint32_t*>(win4);
   const size_t len = text.L - text.mis;
   for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
-    const uint32_t at = pos[idx];
+    const uint32_t at = idx < (uint32_t)kDecBlock ? p0 : pl[idx];
     const uint64_t g = gbase + idx;
     FastNum fn;
     if (g < nvals && fast_segment(l32, at + 1 + kWinPad, g, nvals, b0 + at + 1 - text.mis, len, fn)) {
@@ -1295,9 +1339,10 @@ hipError_t launch_exchange_encode_lens(const uint4* mag, const uint8_t* neg, siz
 // 382 us at 8 Mi pairs, the gather's ~100 us eating the count pass's 110;
 // profiles/r03s2_xdec_pair_via_spans_ab.txt.  The party session keeps the
 // span form and reads it in place.)
-size_t xdec_scratch_bytes(size_t len) {  // span counts, scan partials, the slow-path flag
+// span counts, scan partials, the slow-path flag, the spans' colon lists
+size_t xdec_scratch_bytes(size_t len) {
   const size_t nb = blocks_of(len + 16, kDecSpan);
-  return 8 * (nb + 1) + 8 * ((size_t)blocks_of(nb, kScanBlock) + 1) + 8;
+  return 8 * (nb + 1) + 8 * ((size_t)blocks_of(nb, kScanBlock) + 1) + 8 + 8 + 2 * (size_t)kMaxStarts * nb;
 }
 
 hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, uint4* mag,
@@ -1314,11 +1359,12 @@ hipError_t launch_exchange_decode(const char* text, size_t len, size_t npairs, u
   uint64_t* bscan = static_cast<uint64_t*>(scratch);
   uint64_t* bsum = bscan + nb + 1;
   unsigned int* slow = reinterpret_cast<unsigned int*>(bsum + blocks_of(nb, kScanBlock) + 1);
-  AMPH_LAUNCH(k_xdec_count, dim3(blocks_of(nb, kCntWaves)), dim3(64 * kCntWaves), c0, t, bscan, nb, slow);
+  uint16_t* posg = reinterpret_cast<uint16_t*>(((uintptr_t)(slow + 2) + 15) & ~(uintptr_t)15);  // 16-B aligned
+  AMPH_LAUNCH(k_xdec_count, dim3(blocks_of(nb, kCntWaves)), dim3(64 * kCntWaves), c0, t, bscan, nb, slow, posg);
   hipError_t e = scan_u64(bscan, nb, bsum, cm);
   if (e != hipSuccess) return e;
   AMPH_LAUNCH(k_xdec_fast, dim3((unsigned)nb), dim3(kDecBlock), cm, t, bscan, nb, 2 * npairs, mag, neg,
-              slow);
+              slow, (const uint16_t*)posg);
   AMPH_LAUNCH(k_xdec_slow<ScanBases>, dim3((unsigned)std::min<size_t>(nb, kSlowGrid)), dim3(kDecBlock), c1, t,
               ScanBases{bscan, nb}, nb, 2 * npairs, mag, neg, bad, (const unsigned int*)slow);
   return hipGetLastError();

@@ -595,6 +595,34 @@ def test_exchange_decode_every_length_and_the_2_128_edge(ctx):
             ctx.exchange_decode(t2, len(p2))
 
 
+def test_exchange_decode_dense_spans(ctx):
+    """The count pass's colon list: spans of one-digit values ({"a":1,"b":2},
+    14 bytes a pair: ~1170 values per 8 KiB span, past the list's 256-entry
+    head) next to spans of long ones, at shifted offsets; then a run of
+    colons (more than a span can list) is rejected."""
+    rng = np.random.default_rng(17)
+    pairs = []
+    for blk in range(12):  # alternating dense and sparse stretches
+        n = 1500 if blk % 2 == 0 else 300
+        big = blk % 2 == 1
+        for _ in range(n):
+            a, b = (int(x) for x in rng.integers(-9, 10, 2)) if not big else \
+                (int(rng.integers(0, 2 ** 62)) * 2 ** 64 - 5, -int(rng.integers(0, 2 ** 63)))
+            pairs.append((a, b))
+    text = json.dumps([{"a": a, "b": b} for a, b in pairs], separators=(",", ":")).encode()
+    mag, neg = _diff_arrays(pairs)
+    neg_exp = neg.copy()
+    neg_exp[(mag == 0).all(axis=2)] = 0
+    for off in (0, 1, 9):
+        m2, n2 = ctx.exchange_decode(b" " * off + text, len(pairs))
+        assert np.array_equal(m2, mag)
+        assert np.array_equal(n2, neg_exp)
+    cut = text.index(b"},", len(text) // 2) + 1
+    flood = text[:cut] + b":" * 9000 + text[cut:]
+    with pytest.raises(ValueError, match="offset"):
+        ctx.exchange_decode(flood, len(pairs))
+
+
 def test_exchange_decode_count_and_brackets(ctx):
     with pytest.raises(ValueError, match="exactly 3 FactorPairs"):
         ctx.exchange_decode(b'[{"a":1,"b":2},{"a":3,"b":4}]', 3)
