@@ -70,6 +70,7 @@ def _load():
     L.amph_strerror.argtypes = [i32]
     L.amph_last_error.restype = C.c_char_p
     L.amph_version.restype = C.c_char_p
+    L.amph_build_id.restype = C.c_char_p
     L.amph_recombine_verify.argtypes = [vp, vp, i32, vp, i64p, u32, vp]
     L.amph_mask_input.argtypes = [vp, vp, i32, vp, sz, vp, i64p, u32, vp]
     L.amph_recombine.argtypes = [vp, C.POINTER(vp), i32, sz, vp, u32, vp]
@@ -126,9 +127,35 @@ def _load():
 
 lib = _load()
 
+
+def build_id() -> str:
+    """The id compiled into the loaded library (amph_build_id)."""
+    return lib.amph_build_id().decode()
+
+
+def tree_build_id() -> str:
+    """The id of the source tree beside the library (tools/build_native.py
+    tree_digest over the same sources, headers, flags and arch)."""
+    root = os.path.dirname(HERE)
+    sys.path.insert(0, os.path.join(root, "tools"))
+    try:
+        import build_native
+    finally:
+        sys.path.pop(0)
+    return build_native.tree_digest()
+
+
+def check_build_id() -> str:
+    """Raise unless the loaded library was built from this tree; returns the id."""
+    got, want = build_id(), tree_build_id()
+    if got != want:
+        raise RuntimeError("libamphora_hip.so carries build id %s but the sources beside it hash to %s: "
+                           "rebuild (__graft_entry__.build())" % (got, want))
+    return got
+
 EXPORTED = ["amph_ctx_create", "amph_ctx_create_multi", "amph_ctx_device_count",
             "amph_ctx_destroy", "amph_ctx_device", "amph_ctx_set_batch_words", "amph_ctx_stats", "amph_strerror",
-            "amph_last_error", "amph_version", "amph_recombine_verify", "amph_mask_input",
+            "amph_last_error", "amph_version", "amph_build_id", "amph_recombine_verify", "amph_mask_input",
             "amph_recombine", "amph_recombine_object", "amph_verify", "amph_verify_message", "amph_mask_words", "amph_mask_word_host",
             "amph_to_gfp", "amph_from_gfp", "amph_convert_share", "amph_odo_pre",
             "amph_open_diffs", "amph_odo_post", "amph_open_post", "amph_synth_odos", "amph_synth_words",
@@ -204,8 +231,10 @@ def byte_len(x) -> int:
     if _is_dev(x):
         return x.numel() * x.element_size()
     if isinstance(x, (bytes, bytearray, memoryview)):
-        return len(x)
-    return int(np.asarray(x).nbytes)
+        return memoryview(x).nbytes
+    # the same conversion words_view makes: the length of the uint8 buffer whose
+    # pointer goes to C (an int64 array is 8x its converted size in nbytes)
+    return int(np.ascontiguousarray(x, dtype=np.uint8).size)
 
 
 def _ptr(x):

@@ -116,7 +116,14 @@ class SecretShareUtil:
 
 
 def _odo_arrays(odos: Sequence[OutputDeliveryObject]):
-    return [tuple(_lib.words_view(f) for f in o.fields()) for o in odos]
+    """Every party's five fields as they are, with their own byte lengths:
+    the C ABI applies recombineObject's copyOfRange rules to ragged parties
+    (client SecretShareUtil.java:75,87-88), so nothing is cut here."""
+    return [tuple(o.fields()) for o in odos]
+
+
+def _words(arrays) -> int:
+    return _lib.byte_len(arrays[0][0]) // WORD_WIDTH  # party 0's word count (:75)
 
 
 def verify_output_delivery_objects(util: SecretShareUtil,
@@ -124,34 +131,56 @@ def verify_output_delivery_objects(util: SecretShareUtil,
     """DefaultAmphoraClient.verifyOutputDeliveryObjects :476-505, fused into one
     kernel (K_RV): 5 recombines + verify, returns the canonical secrets."""
     arrays = _odo_arrays(odos)
-    y, ff = util.context.recombine_verify(arrays)
+    y, ff = _native(util.context.recombine_verify, arrays)
     if ff >= 0:
         _raise_for(util, arrays, ff)
     return unpack(y)
 
 
+def _native(fn, *args):
+    """A C-ABI call whose AMPH_E_RANGE (a party's word starting past the end
+    of its array) is Java's ArrayIndexOutOfBoundsException (IndexError)."""
+    try:
+        return fn(*args)
+    except _lib.AmphoraNativeError as e:
+        if e.status == _lib.AMPH_E_RANGE:
+            raise IndexError(str(e)) from e
+        raise
+
+
 def _raise_for(util: SecretShareUtil, arrays, i: int):
-    # re-render the reference message for word i from its recombined values
-    vals = [unpack(util.context.recombine([a[k][i:i + 1] for a in arrays]))[0] for k in range(5)]
+    """Re-render the reference message for word i from its recombined values:
+    each party's word i is Arrays.copyOfRange(field, 16 i, 16 i + 16) --
+    zero-padded when the party's array ends inside it -- exactly what
+    recombineObject hands fromGfp (amph_recombine_object on those slices)."""
+    lo, hi = WORD_WIDTH * i, WORD_WIDTH * (i + 1)
+    vals = [unpack(util.context.recombine_object([_slice(a[k], lo, hi) for a in arrays]))[0]
+            for k in range(5)]
     y, r, v, w, u = vals
     raise IntegrityVerificationException(util.failure_message(y, r, u, v, w))
+
+
+def _slice(x, lo: int, hi: int):
+    if hasattr(x, "is_cuda"):
+        return x.reshape(-1)[lo:hi]
+    return bytes(memoryview(x).cast("B")[lo:hi]) if not isinstance(x, bytes) else x[lo:hi]
 
 
 def create_masked_input(util: SecretShareUtil, secret: Secret,
                         mask_odos: Sequence[OutputDeliveryObject]) -> MaskedInput:
     """Arithmetic of DefaultAmphoraClient.createSecret :150-160 fused into one
-    kernel (K_MASK): verify the Input Mask ODOs, then maskInput per word."""
+    kernel (K_MASK): verify the Input Mask ODOs, then maskInput per word.
+    More secret words than masks: the C ABI verifies every mask first
+    (:153) and only then reports the length (AMPH_E_LEN), which is the
+    reference's IndexOutOfBoundsException from inputMasks.get(i) (:155-157)."""
     arrays = _odo_arrays(mask_odos)
-    W = arrays[0][0].shape[0]
-    if secret.size() > W:
-        # the reference verifies every mask first (verifyOutputDeliveryObjects
-        # :153) and only then indexes inputMasks.get(i) past the end (:155-157):
-        # a tampered mask set fails verification before the size mismatch shows
-        _, ff = util.context.recombine_verify(arrays)
-        if ff >= 0:
-            _raise_for(util, arrays, ff)
-        raise IndexError("Index %d out of bounds for length %d" % (W, W))
-    masked, ff = util.context.mask_input(arrays, pack(secret.data, util.prime))
+    W = _words(arrays)
+    try:
+        masked, ff = _native(util.context.mask_input, arrays, pack(secret.data, util.prime))
+    except _lib.AmphoraNativeError as e:
+        if e.status == _lib.AMPH_E_LEN and secret.size() > W:
+            raise IndexError("Index %d out of bounds for length %d" % (W, W)) from e
+        raise
     if ff >= 0:
         _raise_for(util, arrays, ff)
     return MaskedInput(secret.secret_id, MaskedInputWords(masked), list(secret.tags))
@@ -191,7 +220,7 @@ def _wire_call(fn, *args, **kw):
 
 def _raise_for_texts(util: SecretShareUtil, texts, i: int):
     # failure path only: decode the fields and render the reference message
-    arrays = [tuple(_lib.words_view(util.context.base64_decode(t)) for t in ts) for ts in texts]
+    arrays = [tuple(util.context.base64_decode(t) for t in ts) for ts in texts]
     _raise_for(util, arrays, i)
 
 

@@ -1135,8 +1135,23 @@ int amph_mask_input(amph_ctx* c, const amph_odo* odos, int n, const uint8_t* sec
   size_t W;
   bool ragged;
   if (int st = odo_words(odos, n, &W, &ragged)) return st;
-  if (n_secrets > W)
+  if (n_secrets > W) {
+    // The reference verifies every mask before it indexes past the last one
+    // (DefaultAmphoraClient.java:153 before :160): a MAC failure outranks the
+    // length error.  Verify all W words (n_secrets = 0), then report.  Device
+    // mode waits for the verdict here -- an error path, so the stream sync
+    // costs nothing a correct call pays.
+    int st = amph_mask_input(c, odos, n, nullptr, 0, nullptr, first_fail, flags, stream);
+    if (st != AMPH_OK) return st;
+    if ((flags & AMPH_F_DEVICE) && first_fail) {
+      HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+      int64_t h = 0;
+      HIP_TRY(hipMemcpy(&h, first_fail, sizeof h, hipMemcpyDeviceToHost));  // kPageableRule
+      if ((uint64_t)h != amph::kNoFail)
+        return fail(AMPH_E_VERIFY, "input mask MAC check failed at word " + std::to_string(h));
+    }
     return fail(AMPH_E_LEN, "more secret words than verified input masks");
+  }
   if (n_secrets && (!secrets || !out_masked)) return fail(AMPH_E_PARAM, "null secrets/output");
   if (ragged) {
     if (flags & AMPH_F_DEVICE)
@@ -2064,7 +2079,23 @@ int amph_mask_input_b64(amph_ctx* c, const amph_odo_b64* odos, int n, size_t wor
   size_t nchars;
   uint32_t pad;
   if (int st = wire_check(odos, n, words, &nchars, &pad)) return st;
-  if (n_secrets > words) return fail(AMPH_E_LEN, "more secret words than verified input masks");
+  if (n_secrets > words) {
+    // as amph_mask_input: the texts decode and every mask verifies before the
+    // length error (DefaultAmphoraClient.java:153 before :160)
+    int st = amph_mask_input_b64(c, odos, n, words, nullptr, 0, nullptr, nullptr, first_fail, bad_char,
+                                 flags, stream);
+    if (st != AMPH_OK) return st;
+    if (flags & AMPH_F_DEVICE) {
+      HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+      int64_t v[2] = {(int64_t)AMPH_NO_FAILURE, (int64_t)AMPH_NO_FAILURE};
+      if (first_fail) HIP_TRY(hipMemcpy(&v[0], first_fail, 8, hipMemcpyDeviceToHost));  // kPageableRule
+      if (bad_char) HIP_TRY(hipMemcpy(&v[1], bad_char, 8, hipMemcpyDeviceToHost));
+      if (v[1] != (int64_t)AMPH_NO_FAILURE) return wire_bad_message(v[1], nchars);
+      if (v[0] != (int64_t)AMPH_NO_FAILURE)
+        return fail(AMPH_E_VERIFY, "input mask MAC check failed at word " + std::to_string(v[0]));
+    }
+    return fail(AMPH_E_LEN, "more secret words than verified input masks");
+  }
   if (n_secrets && !secrets) return fail(AMPH_E_PARAM, "null secrets");
   HIP_TRY(use_device(c->device));
   if (flags & AMPH_F_DEVICE) {

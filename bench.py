@@ -185,6 +185,9 @@ def parse():
     ap.add_argument("--host-parties", type=int, default=3)
     ap.add_argument("--host-steps", type=int, default=3)
     ap.add_argument("--host-warmup", type=int, default=1)
+    ap.add_argument("--host-timeout", type=float, default=120.0,
+                    help="seconds any one collective of the host_memory phase may wait for a peer "
+                         "before the phase is abandoned (the line still prints)")
     a = ap.parse_args()
     if a.workload == "auto":
         a.workload = "c4"
@@ -355,6 +358,115 @@ def _scatter_gather_timed(a, torch, dist, ctx, lib, rank, world, value_resident,
     return res
 
 
+def _read_int(path):
+    try:
+        with open(path) as fh:
+            s = fh.read().strip()
+        return None if s in ("", "max") else int(s)
+    except (OSError, ValueError):
+        return None
+
+
+def memory_limits():
+    """Host memory this process may still use, from the two sources that can
+    end it: the cgroup's limit (v2 `memory.max`, or v1
+    `memory.limit_in_bytes`; usage minus reclaimable inactive file pages) and
+    the host's `MemAvailable`.  AMPH_BENCH_MEM_LIMIT_BYTES /
+    AMPH_BENCH_MEM_AVAILABLE_BYTES replace the probed values (tests inject a
+    small limit; a harness may pin one).  Returns a dict of what was found;
+    `headroom_bytes` is the smaller of the two headrooms (None: nothing
+    known)."""
+    cg_limit = cg_used = None
+    for lim, cur, stat in (("/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory.current",
+                            "/sys/fs/cgroup/memory.stat"),
+                           ("/sys/fs/cgroup/memory/memory.limit_in_bytes",
+                            "/sys/fs/cgroup/memory/memory.usage_in_bytes",
+                            "/sys/fs/cgroup/memory/memory.stat")):
+        cg_limit = _read_int(lim)
+        if cg_limit is not None:
+            if cg_limit >= 1 << 60:  # v1 "unlimited" is a huge number
+                cg_limit = None
+                break
+            cg_used = _read_int(cur) or 0
+            try:
+                with open(stat) as fh:
+                    for ln in fh:
+                        k, _, v = ln.partition(" ")
+                        if k in ("inactive_file", "total_inactive_file"):
+                            cg_used = max(0, cg_used - int(v))
+                            break
+            except (OSError, ValueError):
+                pass
+            break
+    avail = None
+    try:
+        with open("/proc/meminfo") as fh:
+            for ln in fh:
+                if ln.startswith("MemAvailable:"):
+                    avail = int(ln.split()[1]) * 1024
+                    break
+    except (OSError, ValueError, IndexError):
+        pass
+    src = {"limit": "cgroup" if cg_limit is not None else None, "available": "/proc/meminfo"}
+    if os.environ.get("AMPH_BENCH_MEM_LIMIT_BYTES"):
+        cg_limit, cg_used, src["limit"] = int(os.environ["AMPH_BENCH_MEM_LIMIT_BYTES"]), 0, "env"
+    if os.environ.get("AMPH_BENCH_MEM_AVAILABLE_BYTES"):
+        avail, src["available"] = int(os.environ["AMPH_BENCH_MEM_AVAILABLE_BYTES"]), "env"
+    heads = [h for h in ((cg_limit - cg_used) if cg_limit is not None else None, avail) if h is not None]
+    return {"mem_limit_bytes": cg_limit, "mem_limit_used_bytes": cg_used, "mem_available_bytes": avail,
+            "headroom_bytes": min(heads) if heads else None, "source": src}
+
+
+HOST_FIXED_BYTES = 256 << 20  # per rank beyond the arrays: small-call arena, numpy/torch temporaries
+
+
+def host_bytes_per_word(n):
+    """Host footprint of host_memory_phase per word and rank: one n-party ODO
+    set (5 fields) + secrets, plain secrets, masked words and canonical
+    secrets, all page-locked; with page-locked caller arrays the pipeline
+    stages nothing on the host."""
+    return 80 * n + 64
+
+
+def plan_host_words(a, dist, distributed, sync_dev, timeout_s):
+    """How many words each rank streams in host_memory_phase, decided BEFORE
+    anything is allocated: the ranks on this node share its memory, so each
+    may use at most half of the smaller headroom (cgroup limit, MemAvailable)
+    divided by the node's rank count; the size is whole --batch-words
+    batches, at most --host-words, and the ranks agree on the smallest (one
+    all-reduce(MIN)).  Returns (words, record): words 0 means "skip the
+    phase", with the reason in record["skipped"].  A SIGKILL from the OOM
+    killer cannot be caught, so this is the only guard that keeps the line."""
+    import torch
+    lim = memory_limits()
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    per_word = host_bytes_per_word(a.host_parties)
+    want = max(0, a.host_words)
+    unit = max(1, min(a.batch_words, want))  # whole batches (or the whole request when smaller)
+    if lim["headroom_bytes"] is None:
+        words = want
+        budget = None
+    else:
+        budget = lim["headroom_bytes"] // 2 // max(1, local_world)
+        fit = max(0, budget - HOST_FIXED_BYTES) // per_word
+        words = min(want, fit // unit * unit)
+    if distributed:
+        t = torch.tensor([words], dtype=torch.int64, device=sync_dev)
+        guarded_all_reduce(dist, t, dist.ReduceOp.MIN, timeout_s)
+        words = int(t.item())
+    rec = dict(lim, local_world_size=local_world, budget_bytes_per_rank=budget, host_bytes_per_word=per_word,
+               fixed_bytes_per_rank=HOST_FIXED_BYTES, host_words_requested=want, host_words_chosen=words,
+               rule="per rank: min(cgroup headroom, MemAvailable) / 2 / ranks on the node, whole "
+                    "batches, min over ranks")
+    if words < unit:
+        rec["skipped"] = ("host memory: %s B of headroom gives %s B per rank, under one %d-word batch "
+                          "(%d B at %d B/word + %d B fixed)"
+                          % (lim["headroom_bytes"], budget, unit, unit * per_word, per_word,
+                             HOST_FIXED_BYTES))
+        return 0, rec
+    return words, rec
+
+
 def host_memory_phase(a, torch, dist, ctx, rank, world, distributed):
     """PCIe-inclusive rate inside the default line (the
     reference path starts and ends in host memory, DefaultAmphoraClient.java:
@@ -378,8 +490,15 @@ def host_memory_phase(a, torch, dist, ctx, rank, world, distributed):
     sub-object (None elsewhere)."""
     import numpy as np
     from amphora_amd.spdz import TEST_PRIME
-    W, n = a.host_words, a.host_parties
+    n = a.host_parties
     sync_dev = "cuda" if distributed and dist.get_backend() == "nccl" else "cpu"
+    T = a.host_timeout
+    try:
+        W, plan = plan_host_words(a, dist, distributed, sync_dev, T)
+    except Exception as e:  # noqa: BLE001 (a rank left before the plan: abandon, keep the line)
+        return _host_abort(rank, "size agreement", e, T)
+    if not W:
+        return dict(plan) if rank == 0 else None
     arrays, err = [], None
     try:  # allocate + page-lock first; the ranks agree before anything is timed
         odos_h = np.empty((5, n, W, 16), np.uint8)
@@ -396,95 +515,116 @@ def host_memory_phase(a, torch, dist, ctx, rank, world, distributed):
         torch.cuda.empty_cache()
     except Exception as e:  # noqa: BLE001 (page-lock / OOM / HIP error: report, do not lose the line)
         err = "%s: %s" % (type(e).__name__, (str(e).splitlines() or [""])[0][:200])
-    if distributed:
-        f = torch.tensor([1 if err else 0], dtype=torch.int32, device=sync_dev)
-        dist.all_reduce(f, op=dist.ReduceOp.MAX)
-        if f.item() and not err:
-            err = "set-up failed on another rank"
-    if err:
-        for arr in arrays:
-            ctx.host_unregister(arr)
-        return {"skipped": "rank %d: %s" % (rank, err)} if rank == 0 else None
     try:
-        ctx.set_batch_words(a.batch_words)
-        odos = [tuple(odos_h[k, j] for k in range(5)) for j in range(n)]
-        # the link itself, same arrays: pinned HtoD / DtoH copies on one stream
-        src = torch.from_numpy(odos_h.reshape(-1)[:min(1 << 30, odos_h.nbytes)])
-        dst = torch.from_numpy(masked_h.reshape(-1)[:min(1 << 29, masked_h.nbytes)])
-        probe_dev = torch.empty(src.numel(), dtype=torch.uint8, device="cuda")
-
-        def copy_rate(fn, nbytes, reps=3):
-            fn()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(reps):
-                fn()
-            e1.record()
-            e1.synchronize()
-            return reps * nbytes / (e0.elapsed_time(e1) * 1e-3) / 1e9
-
-        htod_link = copy_rate(lambda: probe_dev.copy_(src, non_blocking=True), src.numel())
-        dtoh_link = copy_rate(lambda: dst.copy_(probe_dev[:dst.numel()], non_blocking=True), dst.numel())
-        del probe_dev
-        torch.cuda.empty_cache()
-        ok = True
-        for _ in range(a.host_warmup):
-            ctx.mask_input(odos, sec_h, out=masked_h)
-            ctx.recombine_verify(odos, out=ys_h)
-        masked_h.fill(0)
-        ys_h.fill(0)
-        torch.cuda.synchronize()
         if distributed:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(a.host_steps):
-            _, f1 = ctx.mask_input(odos, sec_h, out=masked_h)
-            _, f2 = ctx.recombine_verify(odos, out=ys_h)
-            ok &= f1 == -1 and f2 == -1
-        torch.cuda.synchronize()
-        if distributed:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        checks = {"honest_verdicts": bool(ok), "secrets_match": bool(np.array_equal(ys_h, plain_h))}
-        idx = np.unique(np.random.default_rng(17).integers(0, W, 4096))
-        R = (1 << 128) % TEST_PRIME
-        good = True
-        for i in idx:
-            s_i = int.from_bytes(sec_h[i].tobytes(), "little")
-            y_i = int.from_bytes(plain_h[i].tobytes(), "little")
-            good &= (((s_i - y_i) % TEST_PRIME) * R % TEST_PRIME).to_bytes(16, "little") == masked_h[i].tobytes()
-        checks["masked_sample_match"] = bool(good)
-        ok = all(checks.values())
-        vals = [el, 0.0 if ok else 1.0, htod_link, dtoh_link]
-        if distributed:
-            t = torch.tensor(vals[:2], dtype=torch.float64, device=sync_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            lk = torch.tensor(vals[2:], dtype=torch.float64, device=sync_dev)
-            dist.all_reduce(lk, op=dist.ReduceOp.MIN)
-            vals = t.tolist() + lk.tolist()
-        el, bad, htod_link, dtoh_link = vals
-        if rank != 0:
-            return None
-        htod_b, dtoh_b = 160 * n + 16, 32  # per word and step: 2 ODO sets + secrets in, 2 outputs out
-        ms = el * 1e3 / a.host_steps
-        htod = htod_b * W * a.host_steps / el / 1e9  # per rank, the slowest rank's time
-        return {"words_per_s": W * world * a.host_steps / el, "ms_per_step": ms,
-                "steps": a.host_steps, "warmup": a.host_warmup,
-                "words_per_rank": W, "parties": n, "batch_words": a.batch_words,
-                "host_bytes_per_step": (htod_b + dtoh_b) * W * world,
-                "host_GBps": (htod_b + dtoh_b) * W * world * a.host_steps / el / 1e9,
-                "htod_GBps_per_rank": round(htod, 2),
-                "link_probe_GBps": {"htod": round(htod_link, 2), "dtoh": round(dtoh_link, 2),
-                                    "bytes": [int(src.numel()), int(dst.numel())],
-                                    "note": "pinned copies of the same arrays (HtoD, DtoH bytes), min over ranks"},
-                "frac_of_link": round(htod / htod_link, 4),
-                "memory": "page-locked caller arrays (amph_host_register), outputs reused across calls",
-                "workload": "C5 per-GPU share: amph_mask_input + amph_recombine_verify from host "
-                            "memory, %d words x %d parties per rank" % (W, n),
-                "verified": bad == 0.0, "verify_checks": checks}
+            f = torch.tensor([1 if err else 0], dtype=torch.int32, device=sync_dev)
+            guarded_all_reduce(dist, f, dist.ReduceOp.MAX, T)
+            if f.item() and not err:
+                err = "set-up failed on another rank"
+        if err:
+            return dict(plan, skipped="rank %d: %s" % (rank, err)) if rank == 0 else None
+        return _host_timed(a, torch, dist, ctx, rank, world, distributed, sync_dev, T, W, n, plan,
+                           odos_h, sec_h, plain_h, masked_h, ys_h, TEST_PRIME)
+    except Exception as e:  # noqa: BLE001 (a collective timed out / a rank failed mid-phase)
+        return _host_abort(rank, "timed section", e, T)
     finally:
         for arr in arrays:
             ctx.host_unregister(arr)
+
+
+def _host_abort(rank, where, e, T):
+    """host_memory_phase gave up after a collective timed out or a call
+    failed: the sub-object says so, and `aborted` makes main() skip the
+    scatter/gather phase and abort the communicator (its state is unknown)
+    while still printing the line.  Every rank returns it (main() reads
+    `aborted` on each)."""
+    return {"skipped": "host phase aborted on rank %d (%s): %s: %s" % (
+                rank, where, type(e).__name__, (str(e).splitlines() or [""])[0][:300]),
+            "aborted": True, "timeout_s": T}
+
+
+def _host_timed(a, torch, dist, ctx, rank, world, distributed, sync_dev, T, W, n, plan,
+                odos_h, sec_h, plain_h, masked_h, ys_h, prime):
+    import numpy as np
+
+    def barrier():
+        torch.cuda.synchronize()
+        if distributed:
+            guarded_all_reduce(dist, torch.zeros(1, dtype=torch.int32, device=sync_dev), dist.ReduceOp.MAX, T)
+
+    ctx.set_batch_words(a.batch_words)
+    odos = [tuple(odos_h[k, j] for k in range(5)) for j in range(n)]
+    # the link itself, same arrays: pinned HtoD / DtoH copies on one stream
+    src = torch.from_numpy(odos_h.reshape(-1)[:min(1 << 30, odos_h.nbytes)])
+    dst = torch.from_numpy(masked_h.reshape(-1)[:min(1 << 29, masked_h.nbytes)])
+    probe_dev = torch.empty(src.numel(), dtype=torch.uint8, device="cuda")
+
+    def copy_rate(fn, nbytes, reps=3):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return reps * nbytes / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+    htod_link = copy_rate(lambda: probe_dev.copy_(src, non_blocking=True), src.numel())
+    dtoh_link = copy_rate(lambda: dst.copy_(probe_dev[:dst.numel()], non_blocking=True), dst.numel())
+    del probe_dev
+    torch.cuda.empty_cache()
+    ok = True
+    for _ in range(a.host_warmup):
+        ctx.mask_input(odos, sec_h, out=masked_h)
+        ctx.recombine_verify(odos, out=ys_h)
+    masked_h.fill(0)
+    ys_h.fill(0)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.host_steps):
+        _, f1 = ctx.mask_input(odos, sec_h, out=masked_h)
+        _, f2 = ctx.recombine_verify(odos, out=ys_h)
+        ok &= f1 == -1 and f2 == -1
+    barrier()
+    el = time.perf_counter() - t0
+    checks = {"honest_verdicts": bool(ok), "secrets_match": bool(np.array_equal(ys_h, plain_h))}
+    idx = np.unique(np.random.default_rng(17).integers(0, W, 4096))
+    R = (1 << 128) % prime
+    good = True
+    for i in idx:
+        s_i = int.from_bytes(sec_h[i].tobytes(), "little")
+        y_i = int.from_bytes(plain_h[i].tobytes(), "little")
+        good &= (((s_i - y_i) % prime) * R % prime).to_bytes(16, "little") == masked_h[i].tobytes()
+    checks["masked_sample_match"] = bool(good)
+    ok = all(checks.values())
+    vals = [el, 0.0 if ok else 1.0, htod_link, dtoh_link]
+    if distributed:
+        t = torch.tensor(vals[:2], dtype=torch.float64, device=sync_dev)
+        guarded_all_reduce(dist, t, dist.ReduceOp.MAX, T)
+        lk = torch.tensor(vals[2:], dtype=torch.float64, device=sync_dev)
+        guarded_all_reduce(dist, lk, dist.ReduceOp.MIN, T)
+        vals = t.tolist() + lk.tolist()
+    el, bad, htod_link, dtoh_link = vals
+    if rank != 0:
+        return None
+    htod_b, dtoh_b = 160 * n + 16, 32  # per word and step: 2 ODO sets + secrets in, 2 outputs out
+    ms = el * 1e3 / a.host_steps
+    htod = htod_b * W * a.host_steps / el / 1e9  # per rank, the slowest rank's time
+    return {"words_per_s": W * world * a.host_steps / el, "ms_per_step": ms,
+            "steps": a.host_steps, "warmup": a.host_warmup,
+            "words_per_rank": W, "parties": n, "batch_words": a.batch_words,
+            "host_bytes_per_step": (htod_b + dtoh_b) * W * world,
+            "host_GBps": (htod_b + dtoh_b) * W * world * a.host_steps / el / 1e9,
+            "htod_GBps_per_rank": round(htod, 2),
+            "link_probe_GBps": {"htod": round(htod_link, 2), "dtoh": round(dtoh_link, 2),
+                                "bytes": [int(src.numel()), int(dst.numel())],
+                                "note": "pinned copies of the same arrays (HtoD, DtoH bytes), min over ranks"},
+            "frac_of_link": round(htod / htod_link, 4),
+            "memory": "page-locked caller arrays (amph_host_register), outputs reused across calls",
+            "memory_plan": plan,
+            "workload": "C5 per-GPU share: amph_mask_input + amph_recombine_verify from host "
+                        "memory, %d words x %d parties per rank" % (W, n),
+            "verified": bad == 0.0, "verify_checks": checks}
 
 
 def host_mode(a, A, torch, ctx, dist=None, rank=0, world=1):
@@ -746,9 +886,18 @@ def dry_run(a, world, rank):
             sg_res = {"skipped": "scatter/gather aborted on rank %d: %s: %s" % (
                           rank, type(e).__name__, (str(e).splitlines() or [""])[0][:300]),
                       "aborted": True, "timeout_s": a.sg_timeout}
-    aborted = bool(sg_res and sg_res.get("aborted"))
+    # host_memory_phase's size decision (the probe, the per-node split, the
+    # agreement over ranks), with nothing allocated
+    hm_plan = None
+    if not a.no_host_phase and not sg_res:
+        try:
+            w, hm_plan = plan_host_words(a, dist, dist.is_initialized(), "cpu", a.host_timeout)
+        except Exception as e:  # noqa: BLE001
+            hm_plan = _host_abort(rank, "size agreement", e, a.host_timeout)
+    aborted = bool(sg_res and sg_res.get("aborted")) or bool(hm_plan and hm_plan.get("aborted"))
     if rank == 0:
         emit({"metric": METRIC, "value": None, "unit": "words/s", "n_gpus": world, "dry_run": True,
+              "host_memory_plan": hm_plan,
               "scatter_gather_round_trip": sg_ok, "scatter_gather": sg_res,
               "per_rank": ranks, "ranks_summary": ranks_summary(ranks, world),
               "world_size": world, "backend": dist.get_backend() if dist.is_initialized() else None,
@@ -792,14 +941,116 @@ def exit_after_abort(code):
     os._exit(code)
 
 
+def _dpm_current(path):
+    """Current level of a pp_dpm_* file ("1: 2400Mhz *") in MHz, or None."""
+    try:
+        with open(path) as fh:
+            for ln in fh:
+                if ln.rstrip().endswith("*"):
+                    v = ln.split(":", 1)[1].strip().rstrip("*").strip().lower()
+                    return float(v.replace("mhz", "").strip())
+    except (OSError, ValueError, IndexError):
+        pass
+    return None
+
+
+def box_state(bus):
+    """One reading of the GPU's clocks, power and temperatures from sysfs
+    (no driver calls; safe beside running kernels): pp_dpm_{sclk,mclk,fclk}
+    current levels, and the hwmon freq*/power*/temp* inputs by label.  Units:
+    MHz, W, degrees C.  {} when the device has no such files."""
+    import glob
+    out = {}
+    if not bus:
+        return out
+    dev = "/sys/bus/pci/devices/%s" % bus
+    for k in ("sclk", "mclk", "fclk", "socclk"):
+        v = _dpm_current("%s/pp_dpm_%s" % (dev, k))
+        if v is not None:
+            out["dpm_%s_mhz" % k] = v
+    for hw in sorted(glob.glob(dev + "/hwmon/hwmon*")):
+        for f in sorted(glob.glob(hw + "/*_input")) + sorted(glob.glob(hw + "/power*_cap")) + \
+                sorted(glob.glob(hw + "/power*_average")):
+            name = os.path.basename(f)
+            kind = name.split("_", 1)[0]
+            base = kind.rstrip("0123456789")
+            if base not in ("freq", "power", "temp"):
+                continue
+            try:
+                raw = int(open(f).read().strip())
+            except (OSError, ValueError):
+                continue
+            label = kind
+            try:
+                label = open("%s/%s_label" % (hw, kind)).read().strip().replace(" ", "_") or kind
+            except OSError:
+                pass
+            suffix = name[len(kind) + 1:]
+            if base == "freq":
+                out["%s_mhz" % label] = raw / 1e6
+            elif base == "power":
+                out["%s_%s_w" % (label, suffix)] = raw / 1e6
+            else:
+                out["%s_c" % label] = raw / 1e3
+    return out
+
+
+class BoxSampler:
+    """Samples box_state() every `period` seconds on a thread while the timed
+    region runs (the reads are sysfs files: the launch loop is not
+    perturbed).  record() gives the readings before and after and, per
+    field, the min / mean / max over the samples taken in between."""
+
+    def __init__(self, bus, period=0.05):
+        import threading
+        self.bus, self.period = bus, period
+        self.samples = []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self.before = self.after = None
+
+    def _run(self):
+        while not self._stop.wait(self.period):
+            self.samples.append(box_state(self.bus))
+
+    def start(self):
+        self.before = box_state(self.bus)
+        if self.before:
+            self._t.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        if self._t.is_alive():
+            self._t.join()
+        self.after = box_state(self.bus)
+        return self
+
+    def record(self):
+        if not self.before:
+            return {"available": False, "note": "no pp_dpm_* / hwmon files for %s" % self.bus}
+        during = {}
+        for k in sorted({k for s in self.samples for k in s}):
+            v = [s[k] for s in self.samples if k in s]
+            during[k] = {"min": min(v), "mean": round(sum(v) / len(v), 3), "max": max(v)}
+        return {"available": True, "before": self.before, "after": self.after, "during": during,
+                "samples": len(self.samples), "period_s": self.period,
+                "source": "/sys/bus/pci/devices/%s (pp_dpm_*, hwmon)" % self.bus}
+
+
+def gpu_identity(torch, local):
+    """(PCI address, UUID) of the GPU this rank drives; (None, None) without one."""
+    if not torch.cuda.is_available():  # (--dry-run on a host without a GPU: no identity)
+        return None, None
+    p = torch.cuda.get_device_properties(local)
+    return ("%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id),
+            str(getattr(p, "uuid", "")))
+
+
 def rank_record(torch, rank, local, wall_s, k_mask_ms, k_rv_ms, words):
     """This rank's identity (PCI address and UUID of the GPU it drove) and
     its own device-resident timings."""
-    bus = uuid = None
-    if torch.cuda.is_available():  # (--dry-run on a host without a GPU: no identity)
-        p = torch.cuda.get_device_properties(local)
-        bus = "%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
-        uuid = str(getattr(p, "uuid", ""))
+    bus, uuid = gpu_identity(torch, local)
     return {"rank": rank, "local_rank": local, "pci_bus_id": bus, "uuid": uuid, "words": words,
             "wall_s": wall_s, "k_mask_ms": round(k_mask_ms, 5), "k_rv_ms": round(k_rv_ms, 5)}
 
@@ -862,6 +1113,14 @@ def main():
         else:
             dist.init_process_group(a.backend, timeout=pg_timeout(a))
 
+    # the library measured is this tree's build (compiled-in id = digest of the
+    # sources that travelled with it); refuse to measure anything else
+    build = {"id": A._lib.build_id(), "tree": A._lib.tree_build_id()}
+    build["match"] = build["id"] == build["tree"]
+    if not build["match"]:
+        sys.exit("bench.py: libamphora_hip.so build id %s != tree digest %s: rebuild first"
+                 % (build["id"], build["tree"]))
+    print("bench.py: libamphora_hip.so build id %s (= tree digest)" % build["id"], file=sys.stderr)
     ctx = A.Context(TEST_PRIME, TEST_R, TEST_RINV, device=local)
     if a.mode == "host":
         host_mode(a, A, torch, ctx, dist, rank, world)
@@ -944,9 +1203,11 @@ def main():
     rv_at = {int((j + 0.75) * a.steps / ns): j for j in range(ns)}
     ev_mask = [(lib.TimingEvent(), lib.TimingEvent()) for _ in range(ns)]
     ev_rv = [(lib.TimingEvent(), lib.TimingEvent()) for _ in range(ns)]
+    sampler = BoxSampler(gpu_identity(torch, local)[0])
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
+    sampler.start()
     t0 = time.perf_counter()
     for s in range(a.steps):
         jm, jr = mask_at.get(s), rv_at.get(s)
@@ -959,11 +1220,16 @@ def main():
     if distributed:
         dist.barrier()
     el = time.perf_counter() - t0
+    sampler.stop()
     t_mask = sum(e0.elapsed_ms(e1) for e0, e1 in ev_mask) / ns  # ms per launch
     t_rv = sum(e0.elapsed_ms(e1) for e0, e1 in ev_rv) / ns
     # which physical GPU this rank drove, and its own timings: every rank's
     # record reaches rank 0 (the reported times stay the max over ranks)
     mine = rank_record(torch, rank, local, el, t_mask, t_rv, W)
+    # the box's clocks / power / temperatures around and during the timed
+    # region: a slower kernel on an unchanged build is then silicon or power,
+    # not code, when the clocks say so
+    mine["box"] = sampler.record()
     ranks = [mine]
     if distributed:
         ranks = [None] * world
@@ -1021,6 +1287,7 @@ def main():
                        "note": "each party's 5 ODO fields are rows of one slab (device-generated)"},
             "world_size": world,
             "backend": dist.get_backend() if distributed else None,
+            "build": build,
             "verified": ok,
             "verify_checks": checks,
             "kernels_ms": {k: round(v, 5) for k, v in kern.items()},
@@ -1056,16 +1323,17 @@ def main():
     hm = None
     if not a.no_host_phase:
         hm = host_memory_phase(a, torch, dist, ctx, rank, world, distributed)
-        if rank == 0 and "verified" in hm:
+        if rank == 0 and hm and "verified" in hm:
             ok = ok and hm["verified"]
+    host_aborted = bool(hm and hm.get("aborted"))
     sg = None
-    if distributed and a.scaling == "strong" and not a.no_scatter_gather:
+    if distributed and a.scaling == "strong" and not a.no_scatter_gather and not host_aborted:
         sg = scatter_gather_phase(a, A, torch, dist, ctx, rank, world, resident)
         if rank == 0 and sg and "verified" in sg:
             ok = ok and sg["verified"]
-    aborted = bool(sg and sg.get("aborted"))
+    aborted = host_aborted or bool(sg and sg.get("aborted"))
     if distributed:
-        if not aborted:  # a rank that saw the phase abort tells the others (ranks that finished it
+        if not aborted:  # a rank that saw a phase abort tells the others (ranks that finished it
             # wait here at most --sg-timeout, then abort too)
             flag = torch.zeros(1, dtype=torch.int32, device="cuda" if dist.get_backend() == "nccl" else "cpu")
             try:
@@ -1080,10 +1348,19 @@ def main():
             sg = dict(sg, aborted_after=True)
         if sg is not None:
             line["scatter_gather"] = sg
+        elif host_aborted and a.scaling == "strong" and not a.no_scatter_gather and distributed:
+            line["scatter_gather"] = {"skipped": "not run: the host_memory phase aborted the process group"}
         elif a.scaling == "strong" and not a.no_scatter_gather:
             line["scatter_gather"] = {"skipped": "world size 1: the root's arrays are the only shard, "
                                                  "nothing crosses a link (device-resident value = "
                                                  "this point)"}
+        # phases that were abandoned: `value` and `verified` stand for the
+        # device-resident measurement; these sub-objects carry no number
+        partial = [k for k in ("host_memory", "scatter_gather")
+                   if isinstance(line.get(k), dict) and (line[k].get("aborted") or line[k].get("aborted_after"))]
+        if aborted and not partial:
+            partial = ["process group aborted after the phases"]
+        line["partial"] = partial or None
         # the CPU baseline on rank 0 at EVERY world size, after the GPU work
         if not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)

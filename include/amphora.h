@@ -232,6 +232,11 @@ const char* amph_strerror(int status);
 /* Detail of the last error on the calling thread (empty string if none). */
 const char* amph_last_error(void);
 const char* amph_version(void);
+/* Identity of the build: 16 hex digits of a SHA-256 over the sources and
+ * headers the library is compiled from, the compile flags and the offload
+ * arch (tools/build_native.py tree_digest).  Recomputing it from a source
+ * tree and comparing proves which tree a tested binary came from. */
+const char* amph_build_id(void);
 
 /* ---- client (amphora-java-client) ------------------------------------- */
 /* verifyOutputDeliveryObjects: recombine the 5 fields over n_parties ODOs,
@@ -245,7 +250,11 @@ int amph_recombine_verify(amph_ctx* ctx, const amph_odo* odos, int n_parties,
 /* createSecret arithmetic: verify the Input Mask ODOs as above and write
  * masked[i] = toGfp((secret_i - mask_i) mod p) for i < n_secrets.
  * secrets: LE16 integers (any 128-bit value; reduced mod p).
- * n_secrets must be <= the ODO word count (else AMPH_E_LEN). */
+ * n_secrets must be <= the ODO word count, else AMPH_E_LEN -- but, as in
+ * the reference (DefaultAmphoraClient.java:153 verifies before :160 indexes),
+ * only after all the masks verified: a MAC failure there returns
+ * AMPH_E_VERIFY with *first_fail set, in both modes (device mode waits for
+ * the verdict on this error path). */
 int amph_mask_input(amph_ctx* ctx, const amph_odo* mask_odos, int n_parties,
                     const uint8_t* secrets, size_t n_secrets, uint8_t* out_masked,
                     int64_t* first_fail, uint32_t flags, void* stream);
@@ -401,7 +410,11 @@ int amph_recombine_verify_b64(amph_ctx* ctx, const amph_odo_b64* odos, int n_par
                               uint8_t* out_secrets, int64_t* first_fail, int64_t* bad_char,
                               uint32_t flags, void* stream);
 /* out_masked16 (16 B per secret) and/or out_records24 (24 base64 characters
- * per secret, MaskedInputData's value; device: 16-byte aligned) may be NULL. */
+ * per secret, MaskedInputData's value; device: 16-byte aligned) may be NULL.
+ * n_secrets > words: the texts are decoded and every mask verified first (a
+ * bad character or a MAC failure is reported as such, as the reference
+ * decodes and verifies before it indexes, DefaultAmphoraClient.java:153-160),
+ * and only then AMPH_E_LEN; device mode waits for the verdicts on that path. */
 int amph_mask_input_b64(amph_ctx* ctx, const amph_odo_b64* mask_odos, int n_parties, size_t words,
                         const uint8_t* secrets, size_t n_secrets, uint8_t* out_masked16,
                         char* out_records24, int64_t* first_fail, int64_t* bad_char, uint32_t flags,

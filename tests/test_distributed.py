@@ -262,3 +262,51 @@ def test_scatter_gather_phase_skips_together_when_setup_fails(tmp_path):
     r1 = json.load(open(tmp_path / "r1"))
     assert set(r0) == {"skipped"} and r0["skipped"].startswith("setup failed on rank 0: ")
     assert set(r1) == {"skipped"}
+
+
+def _dry_line(extra, env_extra, gpus=2):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    argv = [sys.executable, os.path.join(root, "bench.py"), "--dry-run"]
+    if gpus > 1:
+        argv += ["--gpus", str(gpus), "--backend", "gloo", "--same-device"]
+    r = subprocess.run(argv + extra, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_host_phase_sizes_itself_to_the_memory_limit():
+    """host_memory_phase decides its per-rank size before allocating (VERDICT
+    r5 item 1): half the smaller headroom (cgroup limit, MemAvailable),
+    split over the node's ranks, in whole batches, agreed over ranks.  An
+    injected limit that fits two 4 Mi-word batches per rank (3 parties, 2
+    ranks) shrinks the 32 Mi-word request to 8 Mi; the line still prints."""
+    per_word, fixed, batch = 80 * 3 + 64, 256 << 20, 4 << 20
+    limit = 2 * 2 * (2 * batch * per_word + fixed) + batch * per_word  # < 3 batches per rank
+    line = _dry_line([], {"AMPH_BENCH_MEM_LIMIT_BYTES": str(limit)})
+    plan = line["host_memory_plan"]
+    assert plan["source"]["limit"] == "env" and plan["mem_limit_bytes"] == limit
+    assert plan["local_world_size"] == 2 and plan["host_bytes_per_word"] == per_word
+    assert plan["host_words_requested"] == 32 << 20 and plan["host_words_chosen"] == 2 * batch
+    assert "skipped" not in plan and plan["mem_available_bytes"] > 0
+    assert line["fault_reported_at"] == line["fault_expected_at"]
+
+
+def test_host_phase_skips_when_one_batch_does_not_fit():
+    """With less headroom than one batch per rank the phase is skipped with
+    the reason and the limits recorded; the rest of the line stands."""
+    line = _dry_line([], {"AMPH_BENCH_MEM_LIMIT_BYTES": str(1 << 30)})
+    plan = line["host_memory_plan"]
+    assert plan["host_words_chosen"] == 0 and plan["skipped"].startswith("host memory: ")
+    assert plan["budget_bytes_per_rank"] == (1 << 30) // 4
+    assert line["scatter_gather_round_trip"] is True and len(line["per_rank"]) == 2
+    # MemAvailable is the other source: the smaller headroom wins
+    line = _dry_line([], {"AMPH_BENCH_MEM_AVAILABLE_BYTES": str(3 << 30)}, gpus=1)
+    plan = line["host_memory_plan"]
+    assert plan["source"]["available"] == "env" and plan["host_words_chosen"] == 4 << 20

@@ -150,6 +150,59 @@ def test_mask_input_fewer_secrets_than_masks(ctx, F):
     assert ff_dev(dff) == -1 and np.array_equal(host(dout), oo)
 
 
+def _oracle_create_secret(F, odos, secrets):
+    """The oracle's createSecret arithmetic (amphora_oracle.py
+    create_secret_masked_inputs, DefaultAmphoraClient.java:150-160): which
+    exception, if any, the reference raises first."""
+    util = O.ClientSecretShareUtil(P, R, RINV)
+    oodos = [O.OutputDeliveryObject(*[f.tobytes() for f in o]) for o in odos]
+    vals = [int.from_bytes(bytes(w), "little") for w in secrets]
+    try:
+        O.create_secret_masked_inputs(util, vals, oodos)
+    except O.IntegrityVerificationException:
+        return "verify"
+    except IndexError:
+        return "index"
+    return "ok"
+
+
+@pytest.mark.parametrize("fault", [450, -1])
+def test_mask_input_more_secrets_than_masks_verifies_first(ctx, F, torch, fault):
+    """with more secret words than masks the C ABI
+    verifies every mask first and returns AMPH_E_VERIFY (first_fail set) for
+    a tampered set, AMPH_E_LEN only for an honest one -- the reference's
+    order (verifyOutputDeliveryObjects :153 before inputMasks.get(i) :160),
+    checked against the oracle, in host and device mode and through the
+    fused wire call."""
+    import amphora_amd as A
+    W, S = 700, 900
+    odos, _ = F.synth_odos(seed=61, n=3, W=W, fault_index=fault)
+    secrets = F.synth_words(seed=62, count=S, mont=False)
+    want = _oracle_create_secret(F, odos, secrets)
+    assert want == ("verify" if fault >= 0 else "index")
+    dodos = [tuple(dev(torch, f) for f in o) for o in odos]
+    texts = [tuple(ctx.base64_encode(f.tobytes()) for f in o) for o in odos]
+    calls = [("host", lambda: ctx.mask_input(odos, secrets), lambda ff: ff),
+             ("device", lambda: ctx.mask_input(dodos, dev(torch, secrets)), ff_dev),
+             ("b64", lambda: ctx.mask_input_b64(texts, W, secrets, records=True)[2], lambda ff: ff)]
+    for mode, call, ffv in calls:
+        if want == "verify":
+            r = call()
+            ff = r[1] if isinstance(r, tuple) else r
+            assert ffv(ff) == fault, mode
+        else:
+            with pytest.raises(A.AmphoraNativeError) as e:
+                call()
+            assert e.value.status == A._lib.AMPH_E_LEN, mode
+    # the client mirror maps the statuses to the reference's exceptions
+    from amphora_amd import client as CL
+    from amphora_amd.entities import IntegrityVerificationException, OutputDeliveryObject, Secret
+    util = CL.SecretShareUtil(ctx)
+    sec = Secret.of([], [int.from_bytes(bytes(w), "little") for w in secrets])
+    with pytest.raises(IntegrityVerificationException if want == "verify" else IndexError):
+        CL.create_masked_input(util, sec, [OutputDeliveryObject(*[f.tobytes() for f in o]) for o in odos])
+
+
 def test_host_batches_report_global_index(ctx, F):
     odos, _ = F.synth_odos(seed=12, n=3, W=2500, fault_index=1777)
     ctx.set_batch_words(1000)

@@ -43,3 +43,25 @@ def test_only_device_resident_launches_count(tmp_path):
         e = got["%s_n%d_w%d" % (k, n, W)]
         assert e["hbm_bytes_per_launch"] == algo[k]
         assert e["ratio_to_algorithmic"] == 1.0
+
+
+def test_launch_size_is_work_items_not_words(tmp_path):
+    """rocprof's Grid_Size counts work-items: ceil(W / block) x block.  A word
+    count that is no multiple of the block still selects its launches, an
+    explicit --grid (a capped grid) selects others, and a run with no
+    matching launch fails naming the sizes it saw."""
+    W, n = 1_000_003, 2
+    grid = -(-W // 256) * 256
+    k = "k_mask"
+    _csv(tmp_path / "f.csv", "FETCH_SIZE", [(grid, k, 10.0)] * 2 + [(4096, k, 99.0)])
+    _csv(tmp_path / "w.csv", "WRITE_SIZE", [(grid, k, 5.0)] * 2 + [(4096, k, 99.0)])
+    out = tmp_path / "t.json"
+    cmd = [sys.executable, str(ROOT / "tools" / "pmc_traffic.py"), str(tmp_path / "f.csv"), str(tmp_path / "w.csv"),
+           "--words", str(W), "--parties", str(n), "--out", str(out)]
+    subprocess.run(cmd, check=True, capture_output=True)
+    assert json.loads(out.read_text())["k_mask_n2_w%d" % W]["hbm_bytes_per_launch"] == (2 * 10.0 + 5.0) * 1024
+    subprocess.run(cmd + ["--grid", "4096"], check=True, capture_output=True)
+    assert json.loads(out.read_text())["k_mask_n2_w%d" % W]["hbm_bytes_per_launch"] == (2 * 99.0 + 99.0) * 1024
+    r = subprocess.run(cmd[:-4] + ["--words", "77", "--parties", str(n), "--out", str(out)], capture_output=True,
+                       text=True)
+    assert r.returncode != 0 and "no FETCH_SIZE launch" in r.stderr and "4096" in r.stderr

@@ -202,3 +202,50 @@ def test_hip_ragged_device_accumulates(gpu):
         assert st == 0
         torch.cuda.synchronize()
         assert int(ff.item()) == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,delta,outcome", CASES)
+def test_client_mirror_ragged_matches_the_reference(gpu, name, delta, outcome):
+    """The Python client mirror (amphora_amd/client.py) hands each party's
+    fields to the C ABI with their real byte lengths, so a ragged partner
+    gives exactly the reference's outcome: the secrets, the
+    IntegrityVerificationException whose message is built from the
+    zero-padded word (copyOfRange), or the index exception -- compared with
+    the oracle's verifyOutputDeliveryObjects / createSecret, message text
+    included (the mirror used to cut the partial word and read
+    past the short party's buffer when rendering the message)."""
+    torch, A, ctx, F = gpu
+    from amphora_amd import client as CL
+    from amphora_amd.entities import IntegrityVerificationException, OutputDeliveryObject, Secret
+    W, n = 37, 3
+    odos = _ragged(F, W, n, delta, seed=41)
+    util = O.ClientSecretShareUtil(P, R, RINV)
+    pyodos = [O.OutputDeliveryObject(*[f.tobytes() for f in o]) for o in odos]
+    codos = [OutputDeliveryObject(*[f.tobytes() for f in o]) for o in odos]
+    cutil = CL.SecretShareUtil(ctx)
+    secrets = [int.from_bytes(w.tobytes(), "little") for w in F.synth_words(seed=42, count=W - 2, mont=False)]
+    for run_ref, run_mirror in (
+            (lambda: O.verify_output_delivery_objects(util, pyodos),
+             lambda: CL.verify_output_delivery_objects(cutil, codos)),
+            (lambda: O.create_secret_masked_inputs(util, secrets, pyodos),
+             lambda: CL.create_masked_input(cutil, Secret.of([], secrets), codos))):
+        if outcome == "range":
+            with pytest.raises(O.ArrayIndexOutOfBoundsException):
+                run_ref()
+            with pytest.raises(IndexError):
+                run_mirror()
+            continue
+        if outcome == "pad":
+            with pytest.raises(O.IntegrityVerificationException) as ref:
+                run_ref()
+            with pytest.raises(IntegrityVerificationException) as got:
+                run_mirror()
+            assert str(got.value) == str(ref.value)
+            continue
+        ref = run_ref()
+        got = run_mirror()
+        if isinstance(got, list):  # canonical secrets
+            assert got == ref
+        else:  # MaskedInput: its words equal the oracle's maskInput bytes
+            assert [bytes(w) for w in got.data.words] == [bytes(x) for x in ref]

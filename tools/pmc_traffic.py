@@ -21,16 +21,38 @@ def kernel_short(name):
     return name.split("(")[0].split("<")[0].split("::")[-1].strip()
 
 
-def per_kernel(path, counter, grid=None):
-    """Average per launch; grid: only launches of that Grid_Size (the
-    default bench line also launches k_mask / k_rv on the host phase's
-    4 Mi-word batches, which must not enter the device-resident figure)."""
+BLOCKS = (64, 128, 256, 512, 1024)
+
+
+def launch_sizes(words, grid=None):
+    """Grid_Size values (work-items) a W-word launch can have: rocprof counts
+    work-items, ceil(W / block) x block for the library's block sizes, or
+    exactly `grid` when given (a grid cap, AMPH_GRID_CAP, makes it smaller)."""
+    if grid is not None:
+        return {grid}
+    return {-(-words // b) * b for b in BLOCKS}
+
+
+def per_kernel(path, counter, words=None, grid=None):
+    """Average per launch over the launches of a W-word call (the default
+    bench line also launches k_mask / k_rv on the host phase's 4 Mi-word
+    batches, which must not enter the device-resident figure).  Fails,
+    naming the sizes it saw, when no launch matches."""
     vals = collections.defaultdict(list)
+    seen = collections.Counter()
+    sizes = launch_sizes(words, grid) if words is not None else None
     for r in csv.DictReader(open(path)):
-        if grid is not None and int(r.get("Grid_Size") or -1) != grid:
+        if r["Counter_Name"] != counter:
             continue
-        if r["Counter_Name"] == counter:
-            vals[kernel_short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+        g = int(r.get("Grid_Size") or -1)
+        k = kernel_short(r["Kernel_Name"])
+        seen[(k, g)] += 1
+        if sizes is not None and g not in sizes:
+            continue
+        vals[k].append(float(r["Counter_Value"]))
+    if not vals:
+        raise SystemExit("%s: no %s launch with Grid_Size in %s; launches seen (kernel, Grid_Size): %s -- "
+                         "pass --grid" % (path, counter, sorted(sizes or []), dict(seen.most_common(8))))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
@@ -40,10 +62,12 @@ def main():
     ap.add_argument("write_csv")
     ap.add_argument("--words", type=int, required=True)
     ap.add_argument("--parties", type=int, required=True)
+    ap.add_argument("--grid", type=int, default=None,
+                    help="the launches' Grid_Size (work-items) when not ceil(W / block) x block")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "traffic.json"))
     a = ap.parse_args()
-    f = per_kernel(a.fetch_csv, "FETCH_SIZE", a.words)
-    w = per_kernel(a.write_csv, "WRITE_SIZE", a.words)
+    f = per_kernel(a.fetch_csv, "FETCH_SIZE", a.words, a.grid)
+    w = per_kernel(a.write_csv, "WRITE_SIZE", a.words, a.grid)
     algo = {"k_rv": 80 * a.parties + 16, "k_mask": 80 * a.parties + 32}
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
     for k in ("k_mask", "k_rv"):
