@@ -141,3 +141,16 @@ def test_out_buffer_validation(native):
             c.recombine_verify(odo, out=bad)
         with pytest.raises(ValueError, match="out must be"):
             c.mask_input(odo, np.zeros((4, 16), np.uint8), out=bad)
+
+
+def test_byte_len_is_the_length_of_what_c_reads(native):
+    """byte_len and words_view agree for every host input form:
+    the length handed to C is the length of the uint8 buffer whose pointer is
+    passed, so an int64 array or a list is never reported at 8x its size."""
+    import numpy as np
+    from amphora_amd._lib import byte_len, words_view
+    for x in (np.arange(40, dtype=np.int64), list(range(40)), bytes(40), bytearray(40),
+              np.zeros(40, np.uint8), memoryview(bytes(40)), np.zeros((5, 8), np.uint16)):
+        v = words_view(x)
+        assert byte_len(x) == 40, type(x)
+        assert v.nbytes == 32 and v.shape == (2, 16)  # whole words of the same buffer
