@@ -689,8 +689,8 @@ __device__ __forceinline__ uint32_t lds_dword(const uint32_t* l32, uint32_t o) {
 // chunks, then the nd % 8 leading digits of the next chunk right-aligned
 // behind '0's.
 template <class AfterOk>
-__device__ __forceinline__ bool fast_parse(const uint32_t* l32, uint32_t o, bool ok, FastNum& r,
-                                           AfterOk after_ok) {
+__device__ __forceinline__ bool fast_parse(const uint32_t* l32, const uint32_t* p10, uint32_t o, bool ok,
+                                           FastNum& r, AfterOk after_ok) {
   const uint32_t first = lds_dword(l32, o);
   r.minus = (first & 0xFFu) == (uint32_t)'-';
   const uint32_t ds = o + (r.minus ? 1u : 0u);
@@ -705,6 +705,7 @@ __device__ __forceinline__ bool fast_parse(const uint32_t* l32, uint32_t o, bool
   const uint32_t full = nd >> 3, rem = nd & 7u;
   bool ovf = false;
   uint32_t v[4];  // (a local, not r.v: in a persistent-loop variant r.v was kept in scratch)
+  uint32_t lo, hi;  // the chunk whose leading rem digits come last
   if (full == 4) {  // 32..39 digits (a random 128-bit value): two 16-digit halves
     const uint64_t p0 = (uint64_t)digits8(d[0], d[1]) * 100000000u + digits8(d[2], d[3]);
     const uint64_t p1 = (uint64_t)digits8(d[4], d[5]) * 100000000u + digits8(d[6], d[7]);
@@ -713,21 +714,24 @@ __device__ __forceinline__ bool fast_parse(const uint32_t* l32, uint32_t o, bool
     v[1] = (uint32_t)(t >> 32);
     v[2] = (uint32_t)(t >> 64);
     v[3] = (uint32_t)(t >> 96);
+    lo = d[8];  // (the common case: no select chain over the registers)
+    hi = d[9];
   } else {
     v[0] = v[1] = v[2] = v[3] = 0;
 #pragma unroll
     for (uint32_t m = 0; m < 4; ++m)
       if (m < full) fold(v, 100000000u, digits8(d[2 * m], d[2 * m + 1]), ovf);
+    lo = d[0];
+    hi = d[1];
+#pragma unroll
+    for (uint32_t m = 1; m < 4; ++m)
+      if (m == full) { lo = d[2 * m]; hi = d[2 * m + 1]; }
   }
   if (rem) {
-    uint32_t lo = d[0], hi = d[1];
-#pragma unroll
-    for (uint32_t m = 1; m < 5; ++m)
-      if (m == full) { lo = d[2 * m]; hi = d[2 * m + 1]; }
     const uint64_t x = ((uint64_t)hi << 32) | lo;
     const uint32_t sh = 8 * (8 - rem);  // 8..56
     const uint64_t y = (x << sh) | (0x3030303030303030ull >> (64 - sh));
-    fold(v, pow10_small(rem), digits8((uint32_t)y, (uint32_t)(y >> 32)), ovf);
+    fold(v, p10[rem], digits8((uint32_t)y, (uint32_t)(y >> 32)), ovf);
   }
   r.v[0] = v[0];
   r.v[1] = v[1];
@@ -802,7 +806,7 @@ __device__ __forceinline__ bool fast_number(const uint32_t* l32, uint32_t o, boo
 // its first byte to its last, so when every value's segment holds, the
 // whole array is well-formed; no neighbour's record is needed.
 // xo: absolute text offset of window offset o; len: the text length.
-__device__ __forceinline__ bool fast_segment(const uint32_t* l32, uint32_t o, uint64_t g,
+__device__ __forceinline__ bool fast_segment(const uint32_t* l32, const uint32_t* p10, uint32_t o, uint64_t g,
                                              size_t nvals, size_t xo, size_t len, FastNum& r) {
   const uint32_t pre = lds_dword(l32, o - 4);
   r.key = (pre >> 8) & 0xFFu;
@@ -814,7 +818,7 @@ __device__ __forceinline__ bool fast_segment(const uint32_t* l32, uint32_t o, ui
     ok = (pre & 0xFFFF00FFu) == 0x3A220022u && (r.key == 'a' || r.key == 'b') && xo == 6 &&
          (lds_dword(l32, o - 6) & 0xFFFFu) == 0x7B5Bu;  // "[{"
   const uint32_t key = r.key;
-  return fast_parse(l32, o, ok, r, [=](uint32_t dend) {
+  return fast_parse(l32, p10, o, ok, r, [=](uint32_t dend) {
     const uint32_t a0 = lds_dword(l32, dend), a1 = lds_dword(l32, dend + 4);
     if ((g & 1) == 0) {
       const uint32_t k = (a0 >> 16) & 0xFFu;
@@ -840,8 +844,8 @@ __device__ __forceinline__ bool fast_segment(const uint32_t* l32, uint32_t o, ui
 // array check adds the count.
 enum : uint32_t { SEG_OK = 1, SEG_M1 = 2, SEG_FIRST = 4, SEG_LAST = 8, SEG_MID = 16 };
 
-__device__ __forceinline__ uint32_t fast_value(const uint32_t* l32, uint32_t o, size_t xo, size_t len,
-                                               FastNum& r) {
+__device__ __forceinline__ uint32_t fast_value(const uint32_t* l32, const uint32_t* p10, uint32_t o, size_t xo,
+                                               size_t len, FastNum& r) {
   const uint32_t pre = lds_dword(l32, o - 5);  // bytes o-5 .. o-2: '{'|',' '"' k '"'
   r.key = (pre >> 16) & 0xFFu;
   const uint32_t lead = pre & 0xFFu;
@@ -857,7 +861,7 @@ __device__ __forceinline__ uint32_t fast_value(const uint32_t* l32, uint32_t o, 
     if ((lds_dword(l32, o - 6) & 0xFFFFu) == 0x7B5Bu) flags |= SEG_FIRST;  // "[{"
   }
   const uint32_t key = r.key;
-  ok = fast_parse(l32, o, ok, r, [&](uint32_t dend) {
+  ok = fast_parse(l32, p10, o, ok, r, [&](uint32_t dend) {
     const uint32_t a0 = lds_dword(l32, dend), a1 = lds_dword(l32, dend + 4);
     if (!m1) {  // NUM ',' '"' K '"' ':', K the other key
       const uint32_t k = (a0 >> 16) & 0xFFu;
@@ -1147,6 +1151,8 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64
                                                      unsigned int* slow, const uint16_t* posg) {
   if ((bscan[nb] & ~kCountMask) != 0) return;  // whitespace somewhere: the general pass does it all
   __shared__ uint4 win4[kWin / 16 + 1];
+  __shared__ uint32_t p10[8];  // 10^k, k < 8: the partial chunk's scale (one LDS read per value)
+  if (threadIdx.x < 8) p10[threadIdx.x] = pow10_small(threadIdx.x);
   // the count pass's colon list (relative to b0); the first 256 read with the
   // window (entries past the span's count are unused)
   static_assert(kListHead == kDecBlock, "one head entry per lane");
@@ -1181,7 +1187,7 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_fast(Text text, const uint64
     const uint32_t at = idx < (uint32_t)kDecBlock ? p0 : pl[idx];
     const uint64_t g = gbase + idx;
     FastNum fn;
-    if (g < nvals && fast_segment(l32, at + 1 + kWinPad, g, nvals, b0 + at + 1 - text.mis, len, fn)) {
+    if (g < nvals && fast_segment(l32, p10, at + 1 + kWinPad, g, nvals, b0 + at + 1 - text.mis, len, fn)) {
       const size_t slot = (g & ~(uint64_t)1) + (fn.key == 'b');
       xst16(mag + slot, make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]));
       neg[slot] = fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0;
@@ -1211,8 +1217,10 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_span(Text text, uint64_t* cn
   if (bad && blockIdx.x == 0 && threadIdx.x == 0) *bad = kNoFail;
   __shared__ uint4 win4[kWin / 16 + 1];
   __shared__ uint16_t pos[kXSpanSlots];  // colon, relative to b0
+  __shared__ uint32_t p10[8];  // 10^k, k < 8: the partial chunk's scale (one LDS read per value)
   __shared__ int sfail;
   if (threadIdx.x == 0) sfail = 0;
+  if (threadIdx.x < 8) p10[threadIdx.x] = pow10_small(threadIdx.x);
   const size_t span = blockIdx.x, b0 = span * kDecSpan;
   const long long w0 = (long long)b0 - kWinPad;
   if (w0 >= (long long)text.mis && w0 + 16LL * (kWin / 16 + 1) <= (long long)text.L) {
@@ -1250,7 +1258,7 @@ __global__ __launch_bounds__(kDecBlock) void k_xdec_span(Text text, uint64_t* cn
   for (uint32_t idx = threadIdx.x; idx < nloc; idx += kDecBlock) {
     const uint32_t at = pos[idx];
     FastNum fn;
-    const uint32_t f = fast_value(l32, at + 1 + kWinPad, b0 + at + 1 - text.mis, len, fn);
+    const uint32_t f = fast_value(l32, p10, at + 1 + kWinPad, b0 + at + 1 - text.mis, len, fn);
     if ((f & SEG_OK) && (span != 0 || idx != 0 || (f & SEG_FIRST))) {
       xst16(dst + idx, make_uint4(fn.v[0], fn.v[1], fn.v[2], fn.v[3]));
       dneg[idx] = (uint8_t)((fn.minus && (fn.v[0] | fn.v[1] | fn.v[2] | fn.v[3]) != 0) | ((fn.key == 'b') << 1));

@@ -1047,11 +1047,27 @@ def gpu_identity(torch, local):
             str(getattr(p, "uuid", "")))
 
 
+def board_identity(bus):
+    """What tells two boards apart when their PCI addresses agree (every
+    1-GPU lease shows the same address): the host name and the board's own
+    sysfs identity (unique_id / serial_number / vbios_version, when readable)."""
+    import socket
+    out = {"host": socket.gethostname()}
+    for k in ("unique_id", "serial_number", "vbios_version", "product_name"):
+        try:
+            v = open("/sys/bus/pci/devices/%s/%s" % (bus, k)).read().strip()
+            if v:
+                out[k] = v
+        except (OSError, TypeError):
+            pass
+    return out
+
+
 def rank_record(torch, rank, local, wall_s, k_mask_ms, k_rv_ms, words):
-    """This rank's identity (PCI address and UUID of the GPU it drove) and
-    its own device-resident timings."""
+    """This rank's identity (PCI address and UUID of the GPU it drove, the
+    host and the board's sysfs identity) and its own device-resident timings."""
     bus, uuid = gpu_identity(torch, local)
-    return {"rank": rank, "local_rank": local, "pci_bus_id": bus, "uuid": uuid, "words": words,
+    return {"rank": rank, "board": board_identity(bus), "local_rank": local, "pci_bus_id": bus, "uuid": uuid, "words": words,
             "wall_s": wall_s, "k_mask_ms": round(k_mask_ms, 5), "k_rv_ms": round(k_rv_ms, 5)}
 
 

@@ -9,6 +9,12 @@
 // lanes 0..47 read the 48 words those units hold -- the same LDS round trip
 // with no s_barrier (a wave's LDS operations complete in order), at the price
 // of 4 consumer waves at 48 lanes where the product has 3 at 64.
+// Result (round 6): per isolated launch -3 % / -6 % (k_mask_b64 / k_rv_b64,
+// profiles/r06_wire_wave_ab.txt; the counters: waits 56.8 -> 48.2 % of wave
+// cycles, VALU +15.6 %, profiles/r06_wire_pmc_wave_ab.json), but +3 % / 0 %
+// in 31 back-to-back launches (ubench_wire_sustained.hip,
+// profiles/r06_wire_wave_sustained_ab.txt): rejected, the product keeps the
+// workgroup buffers.
 #include "../../amphora_amd/csrc/kernels.hip"
 #include "../../amphora_amd/csrc/wire.hip"
 #include "../../amphora_amd/csrc/codec.hip"
