@@ -173,8 +173,8 @@ __device__ __forceinline__ void wire_load(const TextSet& tx, uint4 (&raw)[5][NP 
 }
 
 // K_MASK from the wire, after a tile's fields are summed: verify, mask the
-// secret, and write the masked word and / or its 24-character record (records
-// staged through LDS -- the decode buffers -- and stored as 16-byte runs).
+// secret, and write the masked word and / or its 24-character record (each
+// lane its own, as three nontemporal 8-byte stores).
 template <int NP, int BS>
 __device__ __forceinline__ void mask_tile_out(size_t tile, size_t words, const uint4 s, size_t n_secrets,
                                               W4 (&acc)[5], uint4* out16, char* out24,
@@ -194,26 +194,19 @@ __device__ __forceinline__ void mask_tile_out(size_t tile, size_t words, const u
       enc_word24(m, g);
     }
   }
-  if (!out24) return;
-  // records: 24 B per word through LDS (the two decode buffers, 24 KiB), then
-  // the workgroup's run as 16-byte stores (full workgroups; the last one's
-  // tail per byte)
-  __syncthreads();
-  uint32_t* l = &lds[0][0];
-  if (has_secret)
-#pragma unroll
-    for (int q = 0; q < 6; ++q) l[6 * threadIdx.x + q] = g[q];
-  __syncthreads();
-  const size_t w0 = tile * WW;
-  const size_t nrec = w0 < n_secrets ? min((size_t)WW, n_secrets - w0) : 0;
-  char* dst = out24 + 24 * w0;
-  if (nrec == (size_t)WW) {
-    for (int q = threadIdx.x; q < 6 * WW / 4; q += BS)
-      reinterpret_cast<uint4*>(dst)[q] = make_uint4(l[4 * q], l[4 * q + 1], l[4 * q + 2], l[4 * q + 3]);
-  } else {
-    for (size_t q = threadIdx.x; q < 6 * nrec; q += BS)
-      reinterpret_cast<uint32_t*>(dst)[q] = l[q];
-  }
+  if (!out24 || !has_secret) return;
+  // records: each lane streams its own 24 bytes as three nontemporal 8-byte
+  // stores; a wave's three store instructions cover its 1536 contiguous
+  // bytes, which the L2 merges into whole lines.  Round 5 staged the
+  // workgroup's records in LDS and stored 16-byte runs behind two barriers:
+  // sustained k_mask_b64 277.8 -> 265.6 us at 4 Mi x 3 (plain 8-byte stores:
+  // 274.2), 0.95-0.96 of its access-pattern probe
+  // (profiles/r06_wire_record_stores_ab.txt)
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  u32x2* o = reinterpret_cast<u32x2*>(out24 + 24 * word);
+  __builtin_nontemporal_store(u32x2{g[0], g[1]}, o);
+  __builtin_nontemporal_store(u32x2{g[2], g[3]}, o + 1);
+  __builtin_nontemporal_store(u32x2{g[4], g[5]}, o + 2);
 }
 
 // Waves per SIMD the register allocation must allow (0: the compiler's choice;

@@ -176,8 +176,9 @@ def parse():
                          "`skipped`, the communicator is aborted and the line still prints)")
     ap.add_argument("--pg-timeout", type=float, default=180.0,
                     help="process-group timeout (seconds) for every other collective")
-    ap.add_argument("--inject-sg-fault", choices=["", "error", "hang"], default="",
-                    help=argparse.SUPPRESS)  # tests: rank 1 raises / never posts its gather sends
+    ap.add_argument("--inject-sg-fault", choices=["", "error", "hang", "host-hang"], default="",
+                    help=argparse.SUPPRESS)  # tests: rank 1 raises / never posts its gather sends /
+    # (--dry-run) never joins the host phase's size agreement
     ap.add_argument("--no-host-phase", action="store_true",
                     help="device mode: skip the PCIe-inclusive host_memory sub-object")
     ap.add_argument("--host-words", type=int, default=32 << 20,
@@ -269,7 +270,7 @@ def maybe_inject(inject, rank, world):
     """Test hook (--inject-sg-fault): rank 1 raises ("error") or silently
     skips posting its half of the gather ("hang"), as a stuck RCCL peer
     would.  Returns True when the caller must skip its gather."""
-    if not inject or world < 2 or rank != 1:
+    if inject not in ("error", "hang") or world < 2 or rank != 1:
         return False
     if inject == "error":
         raise RuntimeError("injected scatter/gather fault on rank 1")
@@ -891,6 +892,12 @@ def dry_run(a, world, rank):
     hm_plan = None
     if not a.no_host_phase and not sg_res:
         try:
+            if a.inject_sg_fault == "host-hang" and world > 1 and rank == 1:
+                # a rank stuck before the agreement (as one the OOM killer is
+                # about to take): it never joins; the others give up after
+                # --host-timeout and the line still prints
+                time.sleep(a.host_timeout + 2)
+                raise TimeoutError("injected: rank 1 never joined the host phase")
             w, hm_plan = plan_host_words(a, dist, dist.is_initialized(), "cpu", a.host_timeout)
         except Exception as e:  # noqa: BLE001
             hm_plan = _host_abort(rank, "size agreement", e, a.host_timeout)
@@ -898,6 +905,8 @@ def dry_run(a, world, rank):
     if rank == 0:
         emit({"metric": METRIC, "value": None, "unit": "words/s", "n_gpus": world, "dry_run": True,
               "host_memory_plan": hm_plan,
+              "partial": [k for k, v in (("host_memory", hm_plan), ("scatter_gather", sg_res))
+                          if v and v.get("aborted")] or None,
               "scatter_gather_round_trip": sg_ok, "scatter_gather": sg_res,
               "per_rank": ranks, "ranks_summary": ranks_summary(ranks, world),
               "world_size": world, "backend": dist.get_backend() if dist.is_initialized() else None,

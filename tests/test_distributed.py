@@ -310,3 +310,17 @@ def test_host_phase_skips_when_one_batch_does_not_fit():
     line = _dry_line([], {"AMPH_BENCH_MEM_AVAILABLE_BYTES": str(3 << 30)}, gpus=1)
     plan = line["host_memory_plan"]
     assert plan["source"]["available"] == "env" and plan["host_words_chosen"] == 4 << 20
+
+
+def test_line_survives_a_rank_lost_before_the_host_phase():
+    """A rank that never joins the host phase's size agreement (stuck, or
+    about to be OOM-killed) costs the others --host-timeout, not the line:
+    rank 0 prints it with host_memory aborted and `partial` naming it."""
+    import time
+    t0 = time.time()
+    line = _dry_line(["--inject-sg-fault", "host-hang", "--host-timeout", "5", "--no-scatter-gather"], {})
+    assert time.time() - t0 < 120
+    plan = line["host_memory_plan"]
+    assert plan["aborted"] is True and plan["skipped"].startswith("host phase aborted on rank 0")
+    assert line["partial"] == ["host_memory"]
+    assert line["fault_reported_at"] == line["fault_expected_at"] and len(line["per_rank"]) == 2
