@@ -240,7 +240,7 @@ __global__ __launch_bounds__(kB64Block) void k_b64_encode_blk(const uint8_t* in,
   const uint32_t w[3] = {lds[3 * threadIdx.x], lds[3 * threadIdx.x + 1], lds[3 * threadIdx.x + 2]};
   uint32_t g[4];
   enc_unit12(w, g);
-  *reinterpret_cast<uint4*>(out + 16 * t) = make_uint4(g[0], g[1], g[2], g[3]);
+  st16(out + 16 * t, make_uint4(g[0], g[1], g[2], g[3]));  // (nontemporal: 104.3 -> 99.4 us per 256 MiB)
 }
 
 // (the last workgroup: the remaining units, as k_b64_encode_blk)
@@ -265,6 +265,9 @@ __global__ __launch_bounds__(kB64Block) void k_b64_decode_blk(const char* in, ui
   lds[3 * threadIdx.x + 1] = o[1];
   lds[3 * threadIdx.x + 2] = o[2];
   __syncthreads();
+  // plain stores: the decoded bytes are what the next kernel reads, and
+  // nontemporal ones measured 94.5 -> 100.1 us per 256 MiB back to back
+  // (profiles/r06_codec_store_policy_ab.txt)
   uint4* dst = reinterpret_cast<uint4*>(out + 12 * u0);
   for (int q = threadIdx.x; q < 3 * kB64Block / 4; q += kB64Block)
     dst[q] = make_uint4(lds[4 * q], lds[4 * q + 1], lds[4 * q + 2], lds[4 * q + 3]);
@@ -272,7 +275,8 @@ __global__ __launch_bounds__(kB64Block) void k_b64_decode_blk(const char* in, ui
 
 // Per-word records through LDS: the block's 256 x 24 output chars move as
 // 384 coalesced 16-B stores (the per-lane kernel stores 8 B at a 24-B lane
-// stride): 3.74 -> 4.86 TB/s at 16 Mi words.
+// stride): 3.74 -> 4.86 TB/s at 16 Mi words (round 1; 6.1 -> 6.45 TB/s
+// sustained with the stores nontemporal, round 6).
 // (words % 256 != 0: the last workgroup codes the remaining words per lane)
 __global__ __launch_bounds__(kB64Block) void k_b64_words_blk(const uint4* in, char* out, size_t words) {
   if ((size_t)(blockIdx.x + 1) * kB64Block > words) {
@@ -294,9 +298,12 @@ __global__ __launch_bounds__(kB64Block) void k_b64_words_blk(const uint4* in, ch
 #pragma unroll
   for (int q = 0; q < 6; ++q) lds[6 * threadIdx.x + q] = g[q];
   __syncthreads();
+  // nontemporal 16-byte runs: 110.5 -> 104.1 us per 16 Mi words; each lane's
+  // own record as three nontemporal 8-byte stores (what k_mask_b64 now does,
+  // wire.hip) took 120.2 here (profiles/r06_codec_store_policy_ab.txt)
   uint4* dst = reinterpret_cast<uint4*>(out + 24 * i0);
   for (int q = threadIdx.x; q < 6 * kB64Block / 4; q += kB64Block)
-    dst[q] = make_uint4(lds[4 * q], lds[4 * q + 1], lds[4 * q + 2], lds[4 * q + 3]);
+    st16(dst + q, make_uint4(lds[4 * q], lds[4 * q + 1], lds[4 * q + 2], lds[4 * q + 3]));
 }
 
 // Several equal-length byte streams (the five ODO fields of a party session)
