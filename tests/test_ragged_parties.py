@@ -249,3 +249,40 @@ def test_client_mirror_ragged_matches_the_reference(gpu, name, delta, outcome):
             assert got == ref
         else:  # MaskedInput: its words equal the oracle's maskInput bytes
             assert [bytes(w) for w in got.data.words] == [bytes(x) for x in ref]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["host", "device"])
+@pytest.mark.parametrize("name,delta,outcome", CASES)
+def test_hip_mask_input_ragged_more_secrets_than_masks(gpu, mode, name, delta, outcome):
+    """Ragged parties AND more secret words than masks: the outcome the
+    reference reaches first -- copyOfRange's exception, then the MAC check
+    over the zero-padded word, and only then the index error (createSecret,
+    DefaultAmphoraClient.java:153-160) -- as AMPH_E_RANGE / AMPH_E_VERIFY
+    (first_fail W-1) / AMPH_E_LEN, against the oracle."""
+    torch, A, ctx, F = gpu
+    W, n = 37, 3
+    odos = _ragged(F, W, n, delta, seed=43)
+    secrets = F.synth_words(seed=44, count=W + 5, mont=False)
+    util = O.ClientSecretShareUtil(P, R, RINV)
+    pyodos = [O.OutputDeliveryObject(*[f.tobytes() for f in o]) for o in odos]
+    vals = [int.from_bytes(w.tobytes(), "little") for w in secrets]
+    try:
+        O.create_secret_masked_inputs(util, vals, pyodos)
+        want = "none"
+    except O.ArrayIndexOutOfBoundsException:
+        want = "range"
+    except O.IntegrityVerificationException:
+        want = "verify"
+    except IndexError:
+        want = "len"
+    assert want == {"range": "range", "pad": "verify", "ok": "len"}[outcome]
+    args = _on(torch, mode, odos)
+    sec = secrets if mode == "host" else torch.from_numpy(secrets).cuda()
+    if want == "verify":
+        _, ff = ctx.mask_input(args, sec)
+        assert _ff(torch, ff) == W - 1
+    else:
+        with pytest.raises(A.AmphoraNativeError) as e:
+            ctx.mask_input(args, sec)
+        assert e.value.status == (A._lib.AMPH_E_RANGE if want == "range" else A._lib.AMPH_E_LEN)
