@@ -371,12 +371,6 @@ inline std::vector<std::string> maskSecretText(const SecretShareUtil& util, cons
   std::vector<amph_odo_b64> v;
   for (auto& o : maskOdos) v.push_back(o.view());
   const size_t W = maskOdos.empty() ? 0 : wordsOfBase64(maskOdos[0].f[0]);
-  if (secret.size() > W) {
-    // the reference verifies every mask first (verifyOutputDeliveryObjects,
-    // DefaultAmphoraClient.java:153) and only then indexes past the masks (:155-157)
-    verifyOutputDeliveryText(util, maskOdos);
-    throw std::out_of_range("Index " + std::to_string(W) + " out of bounds for length " + std::to_string(W));
-  }
   std::vector<u128> s(secret);
   for (auto& x : s) x %= util.getPrime();
   Bytes in = packWords(s);
@@ -386,6 +380,10 @@ inline std::vector<std::string> maskSecretText(const SecretShareUtil& util, cons
                                      nullptr, &rec[0], &ff, &bad, 0, nullptr);
   if (st == AMPH_E_PARAM && bad >= 0) throw AmphoraClientException(amph_last_error());
   if (st == AMPH_E_VERIFY) verifyOutputDeliveryText(util, maskOdos);  // throws with the message
+  // more secret words than masks: the ABI has verified every mask first
+  // (DefaultAmphoraClient.java:153 before :155-157), so this is an honest set
+  if (st == AMPH_E_LEN && s.size() > W)
+    throw std::out_of_range("Index " + std::to_string(W) + " out of bounds for length " + std::to_string(W));
   check(st);
   std::vector<std::string> out;
   for (size_t i = 0; i < s.size(); ++i) out.push_back(rec.substr(24 * i, 24));
