@@ -248,13 +248,17 @@ def create_masked_input_json(util: SecretShareUtil, secret: Secret, odo_bodies: 
     launch (amph_mask_input_b64)."""
     from . import wire
     texts, W = _texts_and_words(odo_bodies)
-    if secret.size() > W:  # verify first, then the index error (as create_masked_input)
-        _, ff, _ = _wire_call(util.context.recombine_verify_b64, texts, W)
-        if ff >= 0:
-            _raise_for_texts(util, texts, ff)
-        raise IndexError("Index %d out of bounds for length %d" % (W, W))
-    _, rec, ff, _ = _wire_call(util.context.mask_input_b64, texts, W, pack(secret.data, util.prime),
-                               records=True)
+    try:
+        # more secret words than masks: the ABI decodes and verifies every
+        # mask first (a MAC failure comes back as ff), and only then reports
+        # the length -- the reference's order (:153 before :155-157)
+        _, rec, ff, _ = _wire_call(util.context.mask_input_b64, texts, W, pack(secret.data, util.prime),
+                                   records=True)
+    except AmphoraClientException as e:
+        if secret.size() > W and isinstance(e.__cause__, _lib.AmphoraNativeError) \
+                and e.__cause__.status == _lib.AMPH_E_LEN:
+            raise IndexError("Index %d out of bounds for length %d" % (W, W)) from e.__cause__
+        raise
     if ff >= 0:
         _raise_for_texts(util, texts, ff)
     return wire.records_to_masked_input_json(secret.secret_id, rec, secret.tags)

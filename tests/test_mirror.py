@@ -286,6 +286,26 @@ def test_create_secret_more_secrets_than_masks(A, client_util):
         create_masked_input(client_util, secret, [A.OutputDeliveryObject(*x) for x in f])
 
 
+def test_create_secret_json_more_secrets_than_masks(A, client_util):
+    """The same order from the parties' JSON bodies (one fused wire call:
+    amph_mask_input_b64 verifies before it reports the length)."""
+    from amphora_amd import wire
+    from amphora_amd.client import create_masked_input_json
+    rng = random.Random(9)
+    masks = [rng.randrange(P) for _ in range(10)]
+    f = _odos_for(rng, masks)
+    secret = A.Secret.of([], list(range(11)))
+    bodies = [wire.odo_to_json(client_util.context, A.OutputDeliveryObject(*x)) for x in f]
+    with pytest.raises(IndexError):
+        create_masked_input_json(client_util, secret, bodies)
+    w1 = bytearray(f[1][3])
+    w1[16 * 4] ^= 1
+    f[1][3] = bytes(w1)
+    bodies = [wire.odo_to_json(client_util.context, A.OutputDeliveryObject(*x)) for x in f]
+    with pytest.raises(A.IntegrityVerificationException, match="^Verification of secret has failed"):
+        create_masked_input_json(client_util, secret, bodies)
+
+
 @pytest.mark.parametrize("short", ["masks", "triples"])
 def test_short_castor_stream(A, ctx, kat, short):
     """A Castor download with fewer tuples than requested is rejected before
