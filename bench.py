@@ -368,37 +368,74 @@ def _read_int(path):
         return None
 
 
-def memory_limits():
-    """Host memory this process may still use, from the two sources that can
-    end it: the cgroup's limit (v2 `memory.max`, or v1
-    `memory.limit_in_bytes`; usage minus reclaimable inactive file pages) and
-    the host's `MemAvailable`.  AMPH_BENCH_MEM_LIMIT_BYTES /
-    AMPH_BENCH_MEM_AVAILABLE_BYTES replace the probed values (tests inject a
-    small limit; a harness may pin one).  Returns a dict of what was found;
-    `headroom_bytes` is the smaller of the two headrooms (None: nothing
-    known)."""
-    cg_limit = cg_used = None
-    for lim, cur, stat in (("/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory.current",
-                            "/sys/fs/cgroup/memory.stat"),
-                           ("/sys/fs/cgroup/memory/memory.limit_in_bytes",
-                            "/sys/fs/cgroup/memory/memory.usage_in_bytes",
-                            "/sys/fs/cgroup/memory/memory.stat")):
-        cg_limit = _read_int(lim)
-        if cg_limit is not None:
-            if cg_limit >= 1 << 60:  # v1 "unlimited" is a huge number
-                cg_limit = None
-                break
-            cg_used = _read_int(cur) or 0
+def _cgroup_paths(proc_cgroup):
+    """This process's cgroup path for the v2 hierarchy ("0::/path") and for
+    the v1 memory controller ("N:...memory...:/path"), from /proc/self/cgroup."""
+    v2 = v1 = None
+    try:
+        with open(proc_cgroup) as fh:
+            for ln in fh:
+                parts = ln.rstrip("\n").split(":", 2)
+                if len(parts) != 3:
+                    continue
+                if parts[0] == "0" and parts[1] == "":
+                    v2 = parts[2] or "/"
+                elif "memory" in parts[1].split(","):
+                    v1 = parts[2] or "/"
+    except OSError:
+        pass
+    return v2, v1
+
+
+def _cgroup_headroom(base, rel, limit_f, usage_f, stat_keys):
+    """Walk from this process's cgroup up to the hierarchy's root: every
+    ancestor's limit binds, so the headroom is the smallest (limit - usage
+    + reclaimable inactive file pages) along the way.  Returns (limit, used,
+    directory) of the binding level, or None when no level sets a limit."""
+    best = None
+    d = os.path.normpath(base + "/" + (rel or "/").lstrip("/"))
+    base = os.path.normpath(base)
+    while True:
+        lim = _read_int(os.path.join(d, limit_f))
+        if lim is not None and lim < 1 << 60:  # (v1 "unlimited" is a huge number)
+            used = _read_int(os.path.join(d, usage_f)) or 0
             try:
-                with open(stat) as fh:
+                with open(os.path.join(d, "memory.stat")) as fh:
                     for ln in fh:
                         k, _, v = ln.partition(" ")
-                        if k in ("inactive_file", "total_inactive_file"):
-                            cg_used = max(0, cg_used - int(v))
+                        if k in stat_keys:
+                            used = max(0, used - int(v))
                             break
             except (OSError, ValueError):
                 pass
+            if best is None or lim - used < best[0] - best[1]:
+                best = (lim, used, d)
+        if d == base or len(d) <= len(base):
             break
+        d = os.path.dirname(d)
+    return best
+
+
+def memory_limits():
+    """Host memory this process may still use, from the two sources that can
+    end it: its memory cgroup -- the process's own cgroup and every ancestor
+    (v2 `memory.max` / `memory.current`, or v1 `memory.limit_in_bytes` /
+    `memory.usage_in_bytes`; usage minus reclaimable inactive file pages) --
+    and the host's `MemAvailable`.  AMPH_BENCH_MEM_LIMIT_BYTES /
+    AMPH_BENCH_MEM_AVAILABLE_BYTES replace the probed values (tests inject a
+    small limit; a harness may pin one); AMPH_BENCH_CGROUP_ROOT /
+    AMPH_BENCH_PROC_CGROUP point the probe at another tree (tests).  Returns a
+    dict of what was found; `headroom_bytes` is the smaller of the two
+    headrooms (None: nothing known)."""
+    root = os.environ.get("AMPH_BENCH_CGROUP_ROOT", "/sys/fs/cgroup")
+    v2, v1 = _cgroup_paths(os.environ.get("AMPH_BENCH_PROC_CGROUP", "/proc/self/cgroup"))
+    found = None
+    if os.path.exists(os.path.join(root, "cgroup.controllers")) or v2 is not None:
+        found = _cgroup_headroom(root, v2 or "/", "memory.max", "memory.current", ("inactive_file",))
+    if found is None:
+        found = _cgroup_headroom(os.path.join(root, "memory"), v1 or "/", "memory.limit_in_bytes",
+                                 "memory.usage_in_bytes", ("total_inactive_file", "inactive_file"))
+    cg_limit, cg_used, cg_dir = found if found else (None, None, None)
     avail = None
     try:
         with open("/proc/meminfo") as fh:
@@ -408,7 +445,7 @@ def memory_limits():
                     break
     except (OSError, ValueError, IndexError):
         pass
-    src = {"limit": "cgroup" if cg_limit is not None else None, "available": "/proc/meminfo"}
+    src = {"limit": "cgroup %s" % cg_dir if cg_limit is not None else None, "available": "/proc/meminfo"}
     if os.environ.get("AMPH_BENCH_MEM_LIMIT_BYTES"):
         cg_limit, cg_used, src["limit"] = int(os.environ["AMPH_BENCH_MEM_LIMIT_BYTES"]), 0, "env"
     if os.environ.get("AMPH_BENCH_MEM_AVAILABLE_BYTES"):
