@@ -265,12 +265,14 @@ __global__ __launch_bounds__(kB64Block) void k_b64_decode_blk(const char* in, ui
   lds[3 * threadIdx.x + 1] = o[1];
   lds[3 * threadIdx.x + 2] = o[2];
   __syncthreads();
-  // plain stores: the decoded bytes are what the next kernel reads, and
-  // nontemporal ones measured 94.5 -> 100.1 us per 256 MiB back to back
-  // (profiles/r06_codec_store_policy_ab.txt)
+  // nontemporal: in the client pipeline (15 field decodes, then K_RV /
+  // K_MASK reads the words) the download took 0.699 -> 0.671-0.686 ms and
+  // the consumer kernel 0.20 -> 0.19 ms, interleaved on one box; a loop of
+  // this kernel alone over one buffer prefers plain stores (94.5 vs 100.1 us
+  // per 256 MiB), the real sequence does not (profiles/r06_codec_store_policy_ab.txt)
   uint4* dst = reinterpret_cast<uint4*>(out + 12 * u0);
   for (int q = threadIdx.x; q < 3 * kB64Block / 4; q += kB64Block)
-    dst[q] = make_uint4(lds[4 * q], lds[4 * q + 1], lds[4 * q + 2], lds[4 * q + 3]);
+    st16(dst + q, make_uint4(lds[4 * q], lds[4 * q + 1], lds[4 * q + 2], lds[4 * q + 3]));
 }
 
 // Per-word records through LDS: the block's 256 x 24 output chars move as
