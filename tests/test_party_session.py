@@ -51,7 +51,8 @@ def party_inputs(F, n, W, stride=32):
     return shares, masks, triples
 
 
-@pytest.mark.parametrize("n,W,stride", [(2, 777, 32), (3, 5000, 32), (3, 70001, 16), (1, 300, 32)])
+@pytest.mark.parametrize("n,W,stride", [(2, 777, 32), (3, 5000, 32), (3, 70001, 16), (1, 300, 32),
+                                         (5, 3001, 32), (16, 513, 16)])
 def test_session_matches_oracle(ctx, F, n, W, stride):
     shares, masks, triples = party_inputs(F, n, W, stride)
     pre = [F.odo_pre(shares[j], stride, masks[j], triples[j]) for j in range(n)]
@@ -174,6 +175,28 @@ def test_session_partner_text_forms(ctx, F):
         s.close()
 
 
+def test_session_partner_text_forms_many_parties(ctx, F):
+    """Party counts past k_open_post's templated 1-4: six parties (five
+    partners) and sixteen (AMPH_MAX_PARTIES, fifteen partners), the partner
+    texts cycling through the compact (span form), member-swapped (span form)
+    and spaced (pair order) forms, so one finish sums span-form and
+    pair-order partners at a run-time party count."""
+    for n, W in ((6, 6007), (16, 1031)):
+        shares, masks, triples = party_inputs(F, n, W)
+        pre = [F.odo_pre(shares[j], 32, masks[j], triples[j]) for j in range(n)]
+        texts = [ctx.exchange_encode(pre[j][3], pre[j][4]) for j in range(1, n)]
+        forms = [lambda t: t, reorder_text, lambda t: t.replace(b"},{", b"}, {")]
+        opened = F.recombine_diffs([p[3] for p in pre], [p[4] for p in pre])
+        for p0 in (True, False):
+            ow, ou = F.odo_post(opened, triples[0], p0)
+            s = ctx.party_begin(shares[0], 32, masks[0], triples[0], n, want_yrv=False)
+            for slot, t in enumerate(texts, start=1):
+                s.partner(slot, forms[(slot + p0) % 3](t))
+            w, u = s.finish(p0)
+            assert np.array_equal(w, ow) and np.array_equal(u, ou), (n, p0)
+            s.close()
+
+
 def test_session_small_diffs(ctx, F):
     """Triples whose a, b equal the words they are subtracted from: every diff
     is 0, the texts are {"a":0,"b":0} runs (over 1000 values per 8 KiB, more
@@ -203,7 +226,7 @@ def test_session_small_diffs(ctx, F):
     s1.close()
 
 
-@pytest.mark.parametrize("n,W,stride", [(3, 5000, 32), (2, 70001, 16)])
+@pytest.mark.parametrize("n,W,stride", [(3, 5000, 32), (2, 70001, 16), (6, 4099, 32), (16, 257, 16)])
 def test_session_device_mode(ctx, F, n, W, stride):
     """amph_party_*_dev on torch device tensors, texts handed between the
     parties on the device: the five base64 fields equal the host session's /
