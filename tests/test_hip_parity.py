@@ -122,7 +122,7 @@ def test_recombine_verify_vs_c_oracle(ctx, F, n, W):
     assert ff == off == fault and np.array_equal(y, oy)
 
 
-@pytest.mark.parametrize("n,W", [(1, 1000), (2, 262_145), (3, 40_000), (6, 999)])
+@pytest.mark.parametrize("n,W", [(1, 1000), (2, 262_145), (3, 40_000), (6, 999), (16, 4099)])
 def test_mask_input_vs_c_oracle(ctx, F, n, W):
     odos, _ = F.synth_odos(seed=300 + n, n=n, W=W, noncanon_permille=10)
     secrets = F.synth_words(seed=7, count=W, mont=False)
@@ -212,6 +212,29 @@ def test_host_batches_report_global_index(ctx, F):
     finally:
         ctx.set_batch_words(4 << 20)
     assert ff == 1777 and np.array_equal(y, oy)
+
+
+def test_host_batches_sixteen_parties(ctx, F):
+    """AMPH_MAX_PARTIES through the host pipeline: 16 ODOs (80 input streams
+    per batch, 81 with the secrets), several batches, a MAC fault in a later
+    batch and in the verify-only tail of amph_mask_input, against the oracle."""
+    W, S = 9001, 5000
+    odos, _ = F.synth_odos(seed=17, n=16, W=W, noncanon_permille=10)
+    secrets = F.synth_words(seed=18, count=S, mont=False)
+    bad, _ = F.synth_odos(seed=19, n=16, W=W, fault_index=7777)
+    ctx.set_batch_words(2048)
+    try:
+        y, ff = ctx.recombine_verify(odos)
+        m, mf = ctx.mask_input(odos, secrets)
+        _, bff = ctx.recombine_verify(bad)
+        _, bmf = ctx.mask_input(bad, secrets)
+    finally:
+        ctx.set_batch_words(4 << 20)
+    oy, off = F.recombine_verify(odos)
+    om, omf = F.mask_input(secrets, [tuple(f[:S] for f in o) for o in odos])
+    assert ff == off == -1 and np.array_equal(y, oy)
+    assert mf == omf == -1 and np.array_equal(m, om)
+    assert bff == bmf == 7777
 
 
 def test_host_stream_pinned_and_pageable(ctx, F):

@@ -61,7 +61,7 @@ def _rv(ctx, texts, W, mode):
 
 @pytest.mark.parametrize("mode", ["host", "device"])
 @pytest.mark.parametrize("n,W", [(2, 1), (2, 2), (2, 3), (1, 767), (2, 768), (3, 769), (4, 1537),
-                                 (2, 2304), (5, 2000), (2, 100_003), (3, 65_536)])
+                                 (2, 2304), (5, 2000), (2, 100_003), (3, 65_536), (16, 1031)])
 def test_rv_b64_matches_oracle(ctx, F, mode, n, W):
     odos, _ = F.synth_odos(seed=700 + n + W, n=n, W=W, noncanon_permille=20)
     y, ff, bad = _rv(ctx, texts_of(odos), W, mode)
@@ -176,7 +176,7 @@ def test_rv_b64_length_checks(ctx, F):
 
 @pytest.mark.parametrize("mode", ["host", "device"])
 @pytest.mark.parametrize("n,W,S", [(2, 1, 1), (2, 768, 768), (3, 1000, 999), (2, 100_003, 100_003),
-                                   (4, 5000, 3000), (6, 800, 800), (2, 2305, 0)])
+                                   (4, 5000, 3000), (6, 800, 800), (2, 2305, 0), (16, 1031, 700)])
 def test_mask_b64_matches_oracle(ctx, F, mode, n, W, S):
     import torch
     odos, _ = F.synth_odos(seed=1000 + n + W, n=n, W=W, noncanon_permille=10)
