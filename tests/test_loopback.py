@@ -35,7 +35,8 @@ def _cluster(n, seed, exchange_format="json", transport="objects"):
                                                (3, 257, "objects", "objects"), (2, 1000, "json", "json"),
                                                (3, 769, "json", "json"), (2, 1, "json", "json"),
                                                (4, 2, "objects", "json"), (2, 1000, "session", "objects"),
-                                               (3, 769, "session", "json"), (2, 1, "session", "json")])
+                                               (3, 769, "session", "json"), (2, 1, "session", "json"),
+                                               (5, 129, "session", "json"), (16, 33, "json", "json")])
 def test_upload_download_roundtrip(n, W, fmt, transport):
     """fmt: the inter-VCP open carries MultiplicationExchangeObject JSON bodies
     (GPU-coded) or in-memory FactorPair lists.  transport="json": the
